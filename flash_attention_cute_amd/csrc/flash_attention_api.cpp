@@ -1,0 +1,172 @@
+// flash_attention_api.cpp -- torch host API of the gfx950 FlashAttention-2 forward.
+//
+// Host-side mirror of reference csrc/flash_attention_api.cpp:14-141 (same function name, same
+// argument meaning, same TORCH_CHECK messages, same decode q-head packing and stride-preserving
+// output allocation). Differences, all MI355X-side:
+//   * the compute-capability check (reference :17-19) becomes a gfx950 architecture check that is
+//     cached per device instead of two device-attribute queries per call;
+//   * the kernel is reached through the C-ABI of include/fa_gfx950.h (fa_fwd_gfx950), not a C++
+//     template dispatch (reference csrc/kernel_dispatcher.h); runtime errors come back as a
+//     RuntimeError instead of exit() (reference csrc/utils.h:9-18);
+//   * inputs whose base pointer or strides are not 16-byte aligned (the reference silently assumes
+//     alignment, csrc/flash_attention_template.cuh:135-137) are copied to a contiguous buffer.
+#include <torch/extension.h>
+
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime_api.h>
+
+#include <cmath>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "fa_gfx950.h"
+
+namespace flash_attention {
+
+namespace {
+
+bool device_is_gfx950(int device) {
+    static std::mutex mu;
+    static std::vector<int> cache;  // -1 unknown, 0 no, 1 yes
+    std::lock_guard<std::mutex> lock(mu);
+    if ((int)cache.size() <= device) cache.resize(device + 1, -1);
+    if (cache[device] < 0) {
+        hipDeviceProp_t prop;
+        const hipError_t e = hipGetDeviceProperties(&prop, device);
+        TORCH_CHECK(e == hipSuccess, "hipGetDeviceProperties failed: ", hipGetErrorString(e));
+        cache[device] = std::string(prop.gcnArchName).rfind("gfx950", 0) == 0 ? 1 : 0;
+    }
+    return cache[device] == 1;
+}
+
+bool aligned16(const torch::Tensor &t) {
+    if (reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 != 0) return false;
+    for (int i = 0; i < 3; ++i)
+        if (t.stride(i) % 8 != 0 && t.size(i) > 1) return false;
+    return true;
+}
+
+int64_t stride_or_zero(const torch::Tensor &t, int dim) {
+    // a size-1 dimension may carry any stride; the kernel never steps along it
+    return t.size(dim) == 1 ? 0 : t.stride(dim);
+}
+
+}  // namespace
+
+torch::Tensor flash_attention_fwd(torch::Tensor &q, torch::Tensor &k, torch::Tensor &v, float softmax_scale,
+                                  bool causal) {
+    // Check input shape (reference :21-37)
+    TORCH_CHECK(q.dim() == 4 && k.dim() == 4 && v.dim() == 4, "q, k, v must be 4-D [batch, heads, seqlen, dim]");
+    TORCH_CHECK(q.size(0) == k.size(0) && q.size(0) == v.size(0), "q, k, v must have the same batch size");
+    TORCH_CHECK(k.size(1) == v.size(1), "k, v must have the same number of heads");
+    TORCH_CHECK(k.size(2) == v.size(2), "k, v must have the same sequence length");
+    TORCH_CHECK(q.size(3) == k.size(3) && q.size(3) == v.size(3), "q, k, v must have the same hidden dimension");
+    TORCH_CHECK(q.size(0) > 0 && q.size(1) > 0 && q.size(2) > 0 && q.size(3) > 0,
+                "q, k, v must have at least one element");
+    TORCH_CHECK(k.size(2) > 0, "q, k, v must have at least one element");
+    TORCH_CHECK(q.size(1) >= k.size(1),
+                "number of heads in q must be greater or equal to number of heads in k and v");
+    TORCH_CHECK(q.size(1) % k.size(1) == 0, "number of heads in q must be multiple of number of heads in k and v");
+
+    // Check input data type (reference :39-43)
+    TORCH_CHECK(q.dtype() == k.dtype() && q.dtype() == v.dtype(), "q, k, v must have the same data type");
+    TORCH_CHECK(q.dtype() == torch::kHalf || q.dtype() == torch::kBFloat16,
+                "q, k, v only support fp16 or bf16 data type");
+
+    // Check input memory contiguity (reference :45-51)
+    TORCH_CHECK(q.stride(3) == 1, "q must be contiguous in the last dimension");
+    TORCH_CHECK(k.stride(3) == 1, "k must be contiguous in the last dimension");
+    TORCH_CHECK(v.stride(3) == 1, "v must be contiguous in the last dimension");
+
+    // Check kernel constraints (reference :53-59)
+    TORCH_CHECK(q.size(3) % 8 == 0, "hidden dimension must be multiple of 8");
+    TORCH_CHECK(q.size(3) <= 128, "only support hidden dimension <= 128");
+    TORCH_CHECK(q.is_cuda() && k.is_cuda() && v.is_cuda(), "q, k, v must be on CUDA device");
+    TORCH_CHECK(q.device() == k.device() && q.device() == v.device(), "q, k, v must be on the same CUDA device");
+
+    c10::DeviceGuard device_guard(q.device());
+    TORCH_CHECK(device_is_gfx950(q.device().index()),
+                "flash attention (gfx950 build) is only supported on MI355X / gfx950 devices");
+
+    torch::Tensor qx = aligned16(q) ? q : q.contiguous();
+    torch::Tensor kx = aligned16(k) ? k : k.contiguous();
+    torch::Tensor vx = aligned16(v) ? v : v.contiguous();
+
+    int64_t bs = qx.size(0);
+    int64_t head_q = qx.size(1);
+    const int64_t head_kv = kx.size(1);
+    int64_t seqlen_q = qx.size(2);
+    const int64_t seqlen_kv = kx.size(2);
+    const int64_t headdim = qx.size(3);
+    const int64_t head_q_per_group = head_q / head_kv;
+
+    // Decode q-head packing (reference :64-83): with one query row per head, the q-heads of one
+    // kv group become the rows of a single (batch, kv-head) problem so one workgroup serves the
+    // whole group from one K/V stream. Causal masking is dropped, as in the reference (:81).
+    const bool is_pack_head_q = seqlen_q == 1;
+    if (is_pack_head_q) {
+        head_q = head_kv;
+        seqlen_q = seqlen_q * head_q_per_group;
+        causal = false;
+        qx = qx.reshape({bs, head_q, seqlen_q, headdim});
+        if (!aligned16(qx)) qx = qx.contiguous();
+    }
+
+    // stride-preserving output (reference :85): o inherits q's physical layout, so the
+    // transpose(1, 2).reshape(...) of the HF attention caller stays copy-free
+    auto o = torch::empty_like(qx);
+    if (!aligned16(o)) o = torch::empty(qx.sizes(), qx.options());
+
+    fa_fwd_params params;
+    params.q_ptr = qx.data_ptr();
+    params.k_ptr = kx.data_ptr();
+    params.v_ptr = vx.data_ptr();
+    params.o_ptr = o.data_ptr();
+    params.batch_size = bs;
+    params.num_heads_q = head_q;
+    params.num_heads_kv = head_kv;
+    params.seqlen_q = seqlen_q;
+    params.seqlen_kv = seqlen_kv;
+    params.headdim = headdim;
+    // pack path runs as MHA over the packed rows (reference :100)
+    params.head_q_per_group = is_pack_head_q ? 1 : head_q_per_group;
+    params.q_batch_stride = stride_or_zero(qx, 0);
+    params.k_batch_stride = stride_or_zero(kx, 0);
+    params.v_batch_stride = stride_or_zero(vx, 0);
+    params.o_batch_stride = stride_or_zero(o, 0);
+    params.q_head_stride = stride_or_zero(qx, 1);
+    params.k_head_stride = stride_or_zero(kx, 1);
+    params.v_head_stride = stride_or_zero(vx, 1);
+    params.o_head_stride = stride_or_zero(o, 1);
+    params.q_seqlen_stride = stride_or_zero(qx, 2);
+    params.k_seqlen_stride = stride_or_zero(kx, 2);
+    params.v_seqlen_stride = stride_or_zero(vx, 2);
+    params.o_seqlen_stride = stride_or_zero(o, 2);
+    // log2(e) folded into the scale on the host (reference :87)
+    // (float * double -> float, exactly as `softmax_scale *= M_LOG2E` there)
+    softmax_scale *= M_LOG2E;
+    params.softmax_scale = softmax_scale;
+
+    const int dtype = qx.scalar_type() == torch::kHalf ? FA_DTYPE_F16 : FA_DTYPE_BF16;
+    void *stream = c10::hip::getCurrentHIPStream(qx.device().index()).stream();
+    const int rc = fa_fwd_gfx950(&params, dtype, causal ? 1 : 0, stream);
+    TORCH_CHECK(rc == FA_OK, "fa_fwd_gfx950 failed (code ", rc, "): ", fa_last_error());
+
+    if (is_pack_head_q) {
+        head_q = head_kv * head_q_per_group;
+        seqlen_q = seqlen_q / head_q_per_group;
+        o = o.reshape({bs, head_q, seqlen_q, headdim});
+    }
+    if (o.sizes() != q.sizes()) o = o.reshape(q.sizes());
+    return o;
+}
+
+}  // namespace flash_attention
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+    m.def("flash_attention_fwd", &flash_attention::flash_attention_fwd,
+          "FlashAttention-2 forward, hand-written HIP kernel for MI355X / gfx950");
+    m.def("abi_version", []() { return fa_abi_version(); });
+}

@@ -1,0 +1,126 @@
+/*
+ * fa_gfx950.h -- C-ABI boundary of the MI355X (gfx950 / CDNA4) FlashAttention-2
+ * forward operator.
+ *
+ * This header is the drop-in seam that replaces the reference's C++ template
+ * entry point and its parameter struct:
+ *
+ *   reference csrc/flash_attention.h:5-37   struct FlashAttentionParams
+ *   reference csrc/flash_attention.h:39-41  template<T,kHeaddim,IsCausal>
+ *                                           void run_flash_attention(Params&, cudaStream_t)
+ *   reference csrc/kernel_dispatcher.h:20-52 dtype / headdim / causal dispatch
+ *
+ * The reference dispatches at compile time through three nested lambdas and
+ * reaches the kernel through a C++ template; here the whole dispatch is one
+ * plain C function taking the same parameters by pointer plus two runtime
+ * enums, so it can be bound from ctypes / cgo / JNI without C++ name mangling
+ * or torch types.
+ *
+ * Conventions (identical to the reference's FlashAttentionParams):
+ *   - q [B, Hq, Sq, D], k/v [B, Hkv, Sk, D], o [B, Hq, Sq, D]; the last
+ *     dimension is contiguous (stride 1), every other stride is given in
+ *     ELEMENTS, not bytes;
+ *   - softmax_scale is ALREADY multiplied by log2(e) (reference
+ *     csrc/flash_attention_api.cpp:87), the kernel evaluates exp2;
+ *   - head_q_per_group = Hq / Hkv; q-head h reads kv-head h / head_q_per_group
+ *     (reference csrc/flash_attention_template.cuh:157-160);
+ *   - causal masking is bottom-right aligned: key n is visible to query m iff
+ *     n <= m + (Sk - Sq) (reference csrc/mask.cuh:37-39).
+ *   - base pointers must be 16-byte aligned and D % 8 == 0 (every row chunk is
+ *     a 16-byte vector), D <= 128.
+ *
+ * Return values: FA_OK (0) on success, a positive FA_ERR_* code otherwise;
+ * fa_last_error() returns a human-readable message for the calling thread.
+ * The reference kills the process on a CUDA error (csrc/utils.h:9-18); this
+ * ABI reports it instead, and the torch binding turns it into a RuntimeError.
+ */
+#ifndef FA_GFX950_H
+#define FA_GFX950_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FA_GFX950_ABI_VERSION 1
+
+/* Field order mirrors reference csrc/flash_attention.h:5-37. */
+typedef struct fa_fwd_params {
+    const void *q_ptr;
+    const void *k_ptr;
+    const void *v_ptr;
+    void *o_ptr;
+
+    int64_t batch_size;
+    int64_t num_heads_q;
+    int64_t num_heads_kv;
+    int64_t seqlen_q;
+    int64_t seqlen_kv;
+    int64_t headdim;
+
+    int64_t head_q_per_group;
+
+    int64_t q_batch_stride;
+    int64_t k_batch_stride;
+    int64_t v_batch_stride;
+    int64_t o_batch_stride;
+
+    int64_t q_head_stride;
+    int64_t k_head_stride;
+    int64_t v_head_stride;
+    int64_t o_head_stride;
+
+    int64_t q_seqlen_stride;
+    int64_t k_seqlen_stride;
+    int64_t v_seqlen_stride;
+    int64_t o_seqlen_stride;
+
+    float softmax_scale; /* scale * log2(e) */
+} fa_fwd_params;
+
+/* dtype codes (reference csrc/kernel_dispatcher.h:20-34: kHalf, kBFloat16) */
+enum { FA_DTYPE_F16 = 0, FA_DTYPE_BF16 = 1 };
+
+enum {
+    FA_OK = 0,
+    FA_ERR_INVALID_ARGUMENT = 1, /* shape / stride / alignment violation */
+    FA_ERR_UNSUPPORTED = 2,      /* dtype or headdim with no kernel */
+    FA_ERR_LAUNCH = 3,           /* HIP runtime error at launch */
+};
+
+/*
+ * Launch the forward kernel on `stream` (a hipStream_t; NULL = default
+ * stream). Asynchronous: no host synchronisation, no allocation, no global
+ * state, safe under hipGraph capture.
+ * Replaces run_flash_attention<T,128,IsCausal> (reference
+ * csrc/flash_attention_impl.cu:30-49) together with the dispatch of
+ * csrc/kernel_dispatcher.h:20-52.
+ */
+int fa_fwd_gfx950(const fa_fwd_params *params, int dtype, int causal, void *stream);
+
+/*
+ * Validate `params` exactly as fa_fwd_gfx950 does, without touching the
+ * device. Returns FA_OK or the error code fa_fwd_gfx950 would return.
+ */
+int fa_fwd_gfx950_check(const fa_fwd_params *params, int dtype, int causal);
+
+/* Message for the last non-OK return on this thread ("" if none). */
+const char *fa_last_error(void);
+
+/* FA_GFX950_ABI_VERSION of the loaded library. */
+int fa_abi_version(void);
+
+/*
+ * Tile geometry of the kernel that fa_fwd_gfx950 would launch for these
+ * parameters: rows of q per workgroup, keys per KV tile, threads per
+ * workgroup and number of workgroups. Host-only, for schedulers and tests.
+ */
+int fa_fwd_gfx950_geometry(const fa_fwd_params *params, int causal, int64_t *block_m,
+                           int64_t *block_n, int64_t *threads, int64_t *workgroups);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FA_GFX950_H */

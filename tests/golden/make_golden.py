@@ -1,0 +1,99 @@
+"""Generate golden vectors from the REFERENCE's own Python operator (run in the build container only).
+
+The reference CUDA kernel cannot be built here (CUTLASS submodule empty, no nvcc), but its Python
+layer can be imported: ``flash_attention/flash_attention.py`` registers ``flash_attention::forward``
+whose CPU implementation is the reference's defined non-GPU behaviour (reference
+flash_attention/flash_attention.py:6-15, ``F.scaled_dot_product_attention``). This script imports
+that file straight from /root/reference with its JIT loader replaced by a stub (the loader would
+try to compile the CUDA sources; nothing else is replaced), calls the reference op on seeded
+inputs and stores inputs + outputs as fixtures:
+
+  golden_c1.npz      BASELINE config 1: fp32 B1 H2 S128 D64, no mask (seed 0, q, k, v order)
+  golden_small.npz   fp32 / fp16 / bf16 cases, causal and not, Sq == Sk (where the reference's
+                     top-left CPU causal equals the kernel's bottom-right causal)
+  golden_meta.json   the op schema and the reference's error on a GQA call on CPU
+
+No bytecode is written into /root/reference. Re-run with:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import importlib
+import json
+import sys
+import types
+import warnings
+from pathlib import Path
+
+sys.dont_write_bytecode = True
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+REF = Path("/root/reference")
+OUT = Path(__file__).resolve().parent
+
+
+def import_reference_op():
+    pkg = types.ModuleType("flash_attention")
+    pkg.__path__ = [str(REF / "flash_attention")]
+    sys.modules["flash_attention"] = pkg
+    stub = types.ModuleType("flash_attention.load_cpp_extention")
+    stub.load_extension = lambda: None  # the CUDA JIT build is unavailable; CPU path only
+    sys.modules["flash_attention.load_cpp_extention"] = stub
+    return importlib.import_module("flash_attention.flash_attention")
+
+
+def to_np(t: torch.Tensor) -> np.ndarray:
+    if t.dtype == torch.bfloat16:
+        return t.view(torch.int16).numpy().view(np.uint16)  # raw bf16 bits
+    return t.numpy()
+
+
+def main() -> None:
+    ref = import_reference_op()
+    warnings.simplefilter("ignore")
+    schema = str(torch.ops.flash_attention.forward.default._schema)
+
+    # --- config 1 (BASELINE.json configs[0]) -----------------------------------------------
+    torch.manual_seed(0)
+    q = torch.randn(1, 2, 128, 64)
+    k = torch.randn(1, 2, 128, 64)
+    v = torch.randn(1, 2, 128, 64)
+    o = ref.flash_attn_func(q, k, v)
+    np.savez_compressed(OUT / "golden_c1.npz", q=q.numpy(), k=k.numpy(), v=v.numpy(), o=o.numpy(),
+                        scale=np.float32(64 ** -0.5), causal=np.bool_(False))
+
+    # --- small cases --------------------------------------------------------------------------
+    cases = {}
+    spec = [("f32", torch.float32, 1, 2, 128, 64, False), ("f32", torch.float32, 1, 2, 128, 64, True),
+            ("f16", torch.float16, 1, 2, 96, 64, False), ("f16", torch.float16, 1, 2, 96, 64, True),
+            ("f16", torch.float16, 2, 1, 64, 128, True), ("bf16", torch.bfloat16, 1, 2, 80, 64, False),
+            ("bf16", torch.bfloat16, 1, 2, 80, 128, True)]
+    for i, (name, dt, b, h, s, d, causal) in enumerate(spec):
+        torch.manual_seed(100 + i)
+        q = torch.randn(b, h, s, d).to(dt)
+        k = torch.randn(b, h, s, d).to(dt)
+        v = torch.randn(b, h, s, d).to(dt)
+        scale = None if i % 2 == 0 else 0.1
+        o = ref.flash_attn_func(q, k, v, softmax_scale=scale, causal=causal)
+        key = f"case{i}"
+        cases[f"{key}_q"], cases[f"{key}_k"], cases[f"{key}_v"], cases[f"{key}_o"] = map(to_np, (q, k, v, o))
+        cases[f"{key}_meta"] = np.array([b, h, s, d, int(causal)], dtype=np.int64)
+        cases[f"{key}_dtype"] = np.array(name)
+        cases[f"{key}_scale"] = np.float64(d ** -0.5 if scale is None else scale)
+    np.savez_compressed(OUT / "golden_small.npz", **cases)
+
+    # --- error behaviour ------------------------------------------------------------------------
+    try:
+        ref.flash_attn_func(torch.randn(1, 4, 8, 16), torch.randn(1, 2, 8, 16), torch.randn(1, 2, 8, 16))
+        gqa_err = None
+    except RuntimeError as e:
+        gqa_err = str(e).splitlines()[0]
+    meta = {"schema": schema, "cpu_gqa_error": gqa_err, "n_small_cases": len(spec),
+            "generator": "reference flash_attention/flash_attention.py CPU path, torch " + torch.__version__}
+    (OUT / "golden_meta.json").write_text(json.dumps(meta, indent=1) + "\n")
+    print(json.dumps(meta, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,215 @@
+"""GPU parity of the gfx950 kernel against the CPU oracle (and torch SDPA), through the public op.
+
+Every case calls ``flash_attn_func`` (reference flash_attention/flash_attention.py:46-53) on
+cuda:0, i.e. the custom op -> C++ host API -> C-ABI ``fa_fwd_gfx950`` -> HIP kernel, and compares
+with oracle/fa_oracle.c run on the same seeded inputs (same arithmetic widths: fp32 accumulation,
+P rounded to T before P.V). The sweep follows SURVEY.md section 4: dtype x causal x
+{MHA, GQA, MQA} x {Sq == Sk, Sq == 1 (decode pack), Sq < Sk, Sq > Sk} x D x ragged lengths x
+strided (transposed-view) inputs.
+
+Tolerances (written per test):
+  fp16: |gpu - oracle| <= 2e-3 + 2e-3*|oracle|, mean error <= 1e-4
+  bf16: |gpu - oracle| <= 1.6e-2 + 1.6e-2*|oracle|, mean error <= 1e-3
+One output ulp is 9.8e-4 (fp16) / 7.8e-3 (bf16) at |O| ~ 1; the bounds allow the one-ulp flips that
+a different fp32 summation order and the hardware exp2 produce, nothing systematic.
+"""
+from __future__ import annotations
+
+import zlib
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import fa_oracle as O
+from oracle import fa_oracle_c as OC
+
+pytestmark = pytest.mark.gpu
+
+TOL = {torch.float16: (2e-3, 2e-3, 1e-4), torch.bfloat16: (1.6e-2, 1.6e-2, 1e-3)}
+
+
+@pytest.fixture(scope="module")
+def fa(device):
+    import flash_attention_cute_amd as m
+    from flash_attention_cute_amd import flash_attention as fam
+
+    assert fam.flash_attention_cuda is not None, f"gfx950 extension failed to load: {fam._load_error!r}"
+    return m.flash_attn_func
+
+
+def make(b, hq, hkv, sq, sk, d, dtype, seed):
+    g = torch.Generator().manual_seed(seed)
+    q = torch.randn(b, hq, sq, d, generator=g).to(dtype)
+    k = torch.randn(b, hkv, sk, d, generator=g).to(dtype)
+    v = torch.randn(b, hkv, sk, d, generator=g).to(dtype)
+    return q, k, v
+
+
+def check(out_gpu, q, k, v, scale, causal, dtype):
+    ref = OC.forward(q, k, v, scale, causal).float()
+    got = out_gpu.float().cpu()
+    assert got.shape == ref.shape
+    sq, sk = q.shape[2], k.shape[2]
+    keep = torch.from_numpy(~O.fully_masked_rows(sq, sk, causal))
+    fm = ~keep
+    if fm.any():  # rows that see no key are defined as 0
+        assert torch.all(got[:, :, fm, :] == 0)
+    got, ref = got[:, :, keep, :], ref[:, :, keep, :]
+    assert torch.isfinite(got).all()
+    atol, rtol, mean_tol = TOL[dtype]
+    err = (got - ref).abs()
+    bound = atol + rtol * ref.abs()
+    worst = (err - bound).max().item()
+    assert worst <= 0, f"max err {err.max().item():.3e} exceeds bound by {worst:.3e}"
+    assert err.mean().item() <= mean_tol, f"mean err {err.mean().item():.3e}"
+
+
+SHAPES = [  # (B, Hq, Hkv, Sq, Sk)
+    (1, 2, 2, 128, 128),      # MHA, exact tiles
+    (2, 4, 1, 300, 300),      # MQA, ragged (not a multiple of 64 / 256)
+    (1, 8, 2, 1, 257),        # GQA decode -> q-head pack path
+    (1, 4, 2, 100, 333),      # Sq < Sk (bottom-right causal offset)
+    (1, 2, 2, 333, 100),      # Sq > Sk (fully masked rows when causal)
+    (1, 2, 1, 520, 77),       # several q tiles, short kv
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16], ids=["f16", "bf16"])
+@pytest.mark.parametrize("causal", [False, True], ids=["full", "causal"])
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
+@pytest.mark.parametrize("d", [128, 64])
+def test_parity_sweep(fa, device, dtype, causal, shape, d):
+    b, hq, hkv, sq, sk = shape
+    seed = zlib.crc32(repr((shape, d, causal, str(dtype))).encode())
+    q, k, v = make(b, hq, hkv, sq, sk, d, dtype, seed)
+    out = fa(q.to(device), k.to(device), v.to(device), causal=causal)
+    torch.cuda.synchronize()
+    check(out, q, k, v, d ** -0.5, causal, dtype)
+
+
+@pytest.mark.parametrize("d", [8, 40, 72, 96, 120])
+def test_headdims_multiple_of_8(fa, device, d):
+    q, k, v = make(1, 2, 2, 200, 190, d, torch.float16, d)
+    out = fa(q.to(device), k.to(device), v.to(device), causal=True)
+    check(out, q, k, v, d ** -0.5, True, torch.float16)
+
+
+@pytest.mark.parametrize("d", [36, 100])
+def test_headdim_padding_path(fa, device, d):
+    # D % 8 != 0: the python wrapper zero-pads to a multiple of 8 (reference flash_attention.py:26-31)
+    q, k, v = make(1, 2, 2, 130, 130, d, torch.float16, d)
+    out = fa(q.to(device), k.to(device), v.to(device))
+    assert out.shape == q.shape
+    pad = [0, 8 - d % 8]
+    qp, kp, vp = (torch.nn.functional.pad(t, pad) for t in (q, k, v))
+    ref = OC.forward(qp, kp, vp, d ** -0.5, False)[..., :d].float()
+    assert (out.float().cpu() - ref).abs().max().item() < 2e-3
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16], ids=["f16", "bf16"])
+def test_strided_hf_layout(fa, device, dtype):
+    # HF attention passes q/k/v as transpose(1, 2) views of [B, S, H, D] (models/rope_attn_fwd.py:81-85)
+    b, s, hq, hkv, d = 2, 257, 8, 2, 128
+    g = torch.Generator().manual_seed(7)
+    q4 = torch.randn(b, s, hq, d, generator=g).to(dtype)
+    k4 = torch.randn(b, s, hkv, d, generator=g).to(dtype)
+    v4 = torch.randn(b, s, hkv, d, generator=g).to(dtype)
+    qd, kd, vd = (t.to(device).transpose(1, 2) for t in (q4, k4, v4))
+    assert not qd.is_contiguous()
+    out = fa(qd, kd, vd, causal=True)
+    # stride-preserving output: o inherits q's physical [B, S, H, D] layout (api.cpp:85)
+    assert out.stride() == qd.stride()
+    assert out.transpose(1, 2).is_contiguous()
+    check(out, *(t.transpose(1, 2).contiguous() for t in (q4, k4, v4)), d ** -0.5, True, dtype)
+
+
+def test_custom_scale_and_default_scale(fa, device):
+    q, k, v = make(1, 2, 2, 64, 64, 128, torch.float16, 3)
+    out = fa(q.to(device), k.to(device), v.to(device), softmax_scale=0.3)
+    check(out, q, k, v, 0.3, False, torch.float16)
+    out2 = fa(q.to(device), k.to(device), v.to(device))
+    check(out2, q, k, v, 128 ** -0.5, False, torch.float16)
+
+
+def test_online_softmax_rescale_forced(fa, device):
+    # A key aligned with a component shared by every query makes the running max of every row jump
+    # at KV tile 5 (guide rule 26): the O / l rescale branch is taken by all waves at that tile.
+    q, k, v = make(1, 2, 2, 256, 512, 128, torch.float16, 11)
+    u = torch.randn(128, generator=torch.Generator().manual_seed(1))
+    u = u / u.norm()
+    q = (q.float() + 3 * u).to(torch.float16)
+    k[:, :, 5 * 64 + 3, :] = (12 * u).to(torch.float16)
+    v[:, :, 5 * 64 + 3, :] = 3.0
+    out = fa(q.to(device), k.to(device), v.to(device))
+    check(out, q, k, v, 128 ** -0.5, False, torch.float16)
+
+
+def test_against_sdpa_reference_bar(fa, device):
+    # The reference's own accuracy bar (scripts/benchmark_kernel.py:120-123): allclose(atol=1e-3)
+    # against fp32 eager attention, fp16, Sq == Sk so the top-left mask of SDPA equals ours.
+    q, k, v = make(2, 8, 2, 1024, 1024, 128, torch.float16, 5)
+    for causal in (False, True):
+        out = fa(q.to(device), k.to(device), v.to(device), causal=causal)
+        ref = torch.nn.functional.scaled_dot_product_attention(
+            q.to(device).float(), k.to(device).float(), v.to(device).float(), is_causal=causal,
+            enable_gqa=True)
+        assert torch.allclose(out.float(), ref, atol=1e-3), (out.float() - ref).abs().max().item()
+
+
+def test_deterministic(fa, device):
+    q, k, v = (t.to(device) for t in make(2, 8, 8, 777, 777, 128, torch.bfloat16, 9))
+    a = fa(q, k, v, causal=True)
+    b = fa(q, k, v, causal=True)
+    assert torch.equal(a, b)
+
+
+def test_inputs_not_mutated(fa, device):
+    q, k, v = (t.to(device) for t in make(1, 4, 2, 100, 100, 64, torch.float16, 13))
+    c = [t.clone() for t in (q, k, v)]
+    fa(q, k, v, causal=True)
+    assert all(torch.equal(a, b) for a, b in zip((q, k, v), c))
+
+
+def test_errors_are_runtime_errors(fa, device):
+    q = torch.randn(1, 3, 64, 64, device=device, dtype=torch.float16)
+    k = torch.randn(1, 2, 64, 64, device=device, dtype=torch.float16)
+    with pytest.raises(RuntimeError, match="multiple of number of heads"):
+        fa(q, k, k)
+    q32 = torch.randn(1, 2, 64, 64, device=device)
+    with pytest.raises(RuntimeError, match="fp16 or bf16"):
+        fa(q32, q32, q32)
+    big = torch.randn(1, 2, 64, 192, device=device, dtype=torch.float16)
+    with pytest.raises(RuntimeError, match="<= 128"):
+        fa(big, big, big)
+
+
+def test_full_size_configs_sampled(fa, device):
+    """BASELINE configs 2-4 at full size: sampled heads vs the oracle, all heads vs properties."""
+    cfgs = [  # (B, Hq, Hkv, S, dtype, causal)
+        (4, 32, 32, 4096, torch.float16, False),
+        (4, 32, 32, 8192, torch.bfloat16, True),
+        (4, 32, 8, 4096, torch.float16, True),
+    ]
+    for b, hq, hkv, s, dtype, causal in cfgs:
+        torch.manual_seed(0)
+        q = torch.randn(b, hq, s, 128, device=device, dtype=dtype)
+        k = torch.randn(b, hkv, s, 128, device=device, dtype=dtype)
+        v = torch.randn(b, hkv, s, 128, device=device, dtype=dtype)
+        out = fa(q, k, v, causal=causal)
+        torch.cuda.synchronize()
+        # property over every head: each row is a convex combination of V rows
+        vmin = v.float().amin(dim=2, keepdim=True).repeat_interleave(hq // hkv, dim=1)
+        vmax = v.float().amax(dim=2, keepdim=True).repeat_interleave(hq // hkv, dim=1)
+        slack = 1e-2 if dtype == torch.bfloat16 else 2e-3
+        assert torch.isfinite(out).all()
+        assert bool(((out.float() >= vmin - slack) & (out.float() <= vmax + slack)).all())
+        # exact comparison on sampled (batch, head) pairs, including the last batch / head
+        g = hq // hkv
+        for bi, h in [(0, 0), (b - 1, hq - 1)]:
+            kh = h // g
+            qs = q[bi:bi + 1, h:h + 1].cpu()
+            ks = k[bi:bi + 1, kh:kh + 1].cpu()
+            vs = v[bi:bi + 1, kh:kh + 1].cpu()
+            check(out[bi:bi + 1, h:h + 1], qs, ks, vs, 128 ** -0.5, causal, dtype)
+        del q, k, v, out
