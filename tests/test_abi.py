@@ -1,0 +1,128 @@
+"""The C-ABI boundary (include/fa_gfx950.h): the library loads, exports every declared symbol, and
+validates parameters with the documented error codes -- host-only calls, no GPU needed."""
+from __future__ import annotations
+
+import ctypes
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+HEADER = ROOT / "include" / "fa_gfx950.h"
+LIB = ROOT / "flash_attention_cute_amd" / "lib" / "libfa_gfx950.so"
+
+FA_OK, FA_ERR_INVALID_ARGUMENT, FA_ERR_UNSUPPORTED, FA_ERR_LAUNCH = 0, 1, 2, 3
+
+
+class FaFwdParams(ctypes.Structure):
+    _fields_ = ([(n, ctypes.c_void_p) for n in ("q_ptr", "k_ptr", "v_ptr", "o_ptr")]
+                + [(n, ctypes.c_int64) for n in ("batch_size", "num_heads_q", "num_heads_kv", "seqlen_q", "seqlen_kv",
+                                                 "headdim", "head_q_per_group")]
+                + [(f"{t}_{s}_stride", ctypes.c_int64) for s in ("batch", "head", "seqlen") for t in "qkvo"]
+                + [("softmax_scale", ctypes.c_float)])
+
+
+def declared_functions() -> list[str]:
+    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    return re.findall(r"\b(fa_\w+)\s*\(", text)
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not LIB.exists():
+        pytest.skip("libfa_gfx950.so not built (run __graft_entry__.build())")
+    import torch  # noqa: F401  -- same process layout as the product (torch's HIP runtime first)
+
+    return ctypes.CDLL(str(LIB))
+
+
+def test_header_declares_the_boundary():
+    assert set(declared_functions()) == {"fa_fwd_gfx950", "fa_fwd_gfx950_check", "fa_last_error", "fa_abi_version",
+                                         "fa_fwd_gfx950_geometry"}
+
+
+def test_every_declared_symbol_is_exported(lib):
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", str(LIB)], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (fa_\w+)$", out, flags=re.M))
+    assert set(declared_functions()) <= exported
+
+
+def test_struct_layout_matches_header():
+    # 4 pointers + 7 sizes + 12 strides (int64) + float, padded to 8
+    assert ctypes.sizeof(FaFwdParams) == 4 * 8 + 7 * 8 + 12 * 8 + 8
+    assert FaFwdParams.softmax_scale.offset == 4 * 8 + 19 * 8
+
+
+def good_params(**kw) -> FaFwdParams:
+    b, hq, hkv, s, d = 2, 8, 2, 300, 128
+    p = FaFwdParams(q_ptr=0x10000, k_ptr=0x20000, v_ptr=0x30000, o_ptr=0x40000, batch_size=b, num_heads_q=hq,
+                    num_heads_kv=hkv, seqlen_q=s, seqlen_kv=s, headdim=d, head_q_per_group=hq // hkv,
+                    softmax_scale=0.1275)
+    for t, h in (("q", hq), ("k", hkv), ("v", hkv), ("o", hq)):
+        setattr(p, f"{t}_batch_stride", h * s * d)
+        setattr(p, f"{t}_head_stride", s * d)
+        setattr(p, f"{t}_seqlen_stride", d)
+    for key, val in kw.items():
+        setattr(p, key, val)
+    return p
+
+
+def check(lib, p, dtype=0, causal=0):
+    lib.fa_fwd_gfx950_check.restype = ctypes.c_int
+    rc = lib.fa_fwd_gfx950_check(ctypes.byref(p), dtype, causal)
+    lib.fa_last_error.restype = ctypes.c_char_p
+    return rc, lib.fa_last_error().decode()
+
+
+def test_abi_version(lib):
+    lib.fa_abi_version.restype = ctypes.c_int
+    assert lib.fa_abi_version() == 1
+
+
+def test_check_accepts_valid(lib):
+    assert check(lib, good_params()) == (FA_OK, "")
+    assert check(lib, good_params(), dtype=1, causal=1)[0] == FA_OK
+
+
+@pytest.mark.parametrize("kw,code,msg", [
+    ({"headdim": 100}, FA_ERR_INVALID_ARGUMENT, "multiple of 8"),
+    ({"headdim": 136}, FA_ERR_UNSUPPORTED, "<= 128"),
+    ({"head_q_per_group": 3}, FA_ERR_INVALID_ARGUMENT, "head_q_per_group"),
+    ({"seqlen_kv": 0}, FA_ERR_INVALID_ARGUMENT, "at least one element"),
+    ({"q_ptr": 0x10008}, FA_ERR_INVALID_ARGUMENT, "16-byte aligned"),
+    ({"k_seqlen_stride": 132}, FA_ERR_INVALID_ARGUMENT, "multiples of 8"),
+    ({"o_ptr": None}, FA_ERR_INVALID_ARGUMENT, "non-NULL"),
+])
+def test_check_rejects(lib, kw, code, msg):
+    rc, err = check(lib, good_params(**kw))
+    assert rc == code and msg in err
+
+
+def test_check_rejects_dtype(lib):
+    rc, err = check(lib, good_params(), dtype=7)
+    assert rc == FA_ERR_UNSUPPORTED and "dtype" in err
+
+
+def test_null_params(lib):
+    lib.fa_fwd_gfx950_check.restype = ctypes.c_int
+    assert lib.fa_fwd_gfx950_check(None, 0, 0) == FA_ERR_INVALID_ARGUMENT
+
+
+def test_launch_entry_validates_before_touching_the_device(lib):
+    lib.fa_fwd_gfx950.restype = ctypes.c_int
+    p = good_params(headdim=100)
+    assert lib.fa_fwd_gfx950(ctypes.byref(p), 0, 0, None) == FA_ERR_INVALID_ARGUMENT
+
+
+def test_geometry(lib):
+    lib.fa_fwd_gfx950_geometry.restype = ctypes.c_int
+    vals = [ctypes.c_int64() for _ in range(4)]
+    rc = lib.fa_fwd_gfx950_geometry(ctypes.byref(good_params()), 0, *[ctypes.byref(x) for x in vals])
+    assert rc == FA_OK
+    bm, bn, thr, wg = (x.value for x in vals)
+    assert (bm, bn, thr) == (256, 64, 512)
+    assert wg == 2 * 8 * ((300 + bm - 1) // bm)
