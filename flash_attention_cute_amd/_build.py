@@ -55,7 +55,7 @@ def _run(cmd: list[str], verbose: bool) -> None:
 
 
 def abi_sources() -> list[Path]:
-    return [CSRC / "fa_fwd_gfx950.hip", INCLUDE / "fa_gfx950.h"]
+    return [CSRC / "fa_fwd_gfx950.hip", INCLUDE / "fa_gfx950.h", Path(__file__).resolve()]
 
 
 def build_abi(force: bool = False, verbose: bool = False) -> Path:
@@ -67,7 +67,8 @@ def build_abi(force: bool = False, verbose: bool = False) -> Path:
         raise RuntimeError(f"hipcc not found at {HIPCC}")
     tmp = ABI_LIB.with_suffix(".so.tmp")
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-mcode-object-version=5", "-include", "stdarg.h", f"-I{INCLUDE}",
+           "-mcode-object-version=5", "-ffinite-math-only", "-fno-signed-zeros",
+           "-include", "stdarg.h", f"-I{INCLUDE}",
            CSRC / "fa_fwd_gfx950.hip", "-o", tmp]
     _run(cmd, verbose)
     os.replace(tmp, ABI_LIB)

@@ -36,14 +36,17 @@
 
 namespace fa {
 
-constexpr int kBlockM = 256;      // query rows per workgroup
-constexpr int kBlockN = 64;       // keys per KV tile
-constexpr int kHeadDimPad = 128;  // head dim of the LDS image / MFMA k-steps (D <= 128, zero padded)
+constexpr int kBlockM = 256;  // query rows per workgroup
+constexpr int kBlockN = 64;   // keys per KV tile
 constexpr int kWaves = 8;
 constexpr int kThreads = kWaves * 64;
-constexpr int kTileBytes = kBlockN * kHeadDimPad * 2;  // 16 KiB: one K or V tile
-constexpr int kBufBytes = 2 * kTileBytes;              // K + V
-constexpr int kLdsBytes = 2 * kBufBytes;               // double buffer, 64 KiB
+// Masked / not-yet-seen scores use a large finite sentinel instead of -inf so that the kernel can
+// be compiled without IEEE inf/NaN semantics (no canonicalising v_max before fmaxf, v_max3).
+constexpr float kNeg = -1.0e30f;
+// Deferred rescale (guide T13): the running max used for exp2 is only raised when a row's max grows
+// by more than kRescaleThr (log2 units, i.e. a factor 2^8) -- P then stays <= 256, exact in fp16 /
+// bf16 relative precision, and the O / l rescale pass is skipped on almost every tile.
+constexpr float kRescaleThr = 8.0f;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -54,13 +57,19 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+template <int N>
+struct IC {
+    static constexpr int value = N;
+};
 
 struct F16 {
     static __device__ __forceinline__ f32x16 mfma(u32x4 a, u32x4 b, f32x16 c) {
         return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a),
                                                       __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
     }
-    // round-to-nearest-even pack of two fp32 into two fp16 (low element first)
+    // round-to-nearest-even pack of two fp32 into two fp16 (low element first): v_cvt_pk_f16_f32
     static __device__ __forceinline__ uint32_t pack(float lo, float hi) {
         f16x2 v = __builtin_convertvector((f32x2){lo, hi}, f16x2);
         return __builtin_bit_cast(uint32_t, v);
@@ -72,19 +81,38 @@ struct BF16 {
         return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
                                                        __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
     }
+    // v_cvt_pk_bf16_f32 (RNE)
     static __device__ __forceinline__ uint32_t pack(float lo, float hi) {
         bf16x2 v = __builtin_convertvector((f32x2){lo, hi}, bf16x2);
         return __builtin_bit_cast(uint32_t, v);
     }
 };
 
-// K tile image: 64 rows x 256 B; 16-B chunk c of row r lives at chunk slot c ^ (r & 15).
-// The A-operand read (lane r reads row r, one chunk) then hits 16 distinct slots per
-// ds_read_b128 lane group (groups cover rows {0-3,12-15,20-27} etc., distinct mod 16).
-__device__ __forceinline__ int k_off(int row, int ch) { return row * 256 + 16 * (ch ^ (row & 15)); }
-// V tile image: chunk slot c ^ ((r & 3) << 2). A ds_read_b64_tr_b16 half-wave reads 4 rows x
-// 64 B; the XOR moves each of the 4 rows into a different 64-B quarter of the bank row.
-__device__ __forceinline__ int v_off(int row, int ch) { return row * 256 + 16 * (ch ^ ((row & 3) << 2)); }
+// Per head-dim geometry. kD is the padded head dim of the LDS image and of the MFMA k-steps.
+template <int kD>
+struct Geo {
+    static constexpr int kRowBytes = kD * 2;            // 256 / 128
+    static constexpr int kChunks = kD / 8;              // 16-B chunks per row
+    static constexpr int kTileBytes = kBlockN * kRowBytes;
+    static constexpr int kBufBytes = 2 * kTileBytes;    // K + V
+    static constexpr int kLdsBytes = 2 * kBufBytes;     // double buffer
+    static constexpr int kKSteps = kD / 16;             // k-steps of S^T = K.Q^T
+    static constexpr int kDTiles = kD / 32;             // 32-row d tiles of O^T
+    static constexpr int kStage = kBlockN * kChunks / kThreads;  // chunks per thread per tile (2 / 1)
+
+    // K image: the A-operand read has lane r on row r (one 16-B chunk each). For 256-B rows the
+    // chunk slot is c ^ (r & 15); for 128-B rows (two rows per 256-B bank row) c ^ ((r >> 1) & 7).
+    // Both put the 16 lanes of every ds_read_b128 lane group on 16 distinct 16-B bank slots.
+    static __device__ __forceinline__ int k_off(int row, int ch) {
+        return kD == 128 ? row * 256 + 16 * (ch ^ (row & 15)) : row * 128 + 16 * (ch ^ ((row >> 1) & 7));
+    }
+    // V image, read transposed by ds_read_b64_tr_b16: a half-wave reads 4 rows R..R+3 (R % 4 == 0)
+    // x 64 B; the XOR puts the four 64-B pieces into the four quarters of the 256-B bank row.
+    static __device__ __forceinline__ int v_off(int row, int ch) {
+        return kD == 128 ? row * 256 + 16 * (ch ^ ((row & 3) << 2))
+                         : row * 128 + 16 * (ch ^ (((row >> 1) & 1) << 2));
+    }
+};
 
 // v_permlane32_swap(vdst=x, src=x): the lower half-wave receives the upper half's x in the src
 // result and keeps its own in vdst; the upper half the other way round. Combining both results
@@ -104,9 +132,22 @@ __device__ __forceinline__ u32x2 tr_read(const char *lds_ptr) {
     return __builtin_bit_cast(u32x2, v);
 }
 
-template <class DT, bool kCausal>
+// Buffer descriptor over [base, base + nbytes): loads past the end return 0 and stores past the
+// end are dropped by the hardware range check, so ragged tails need no per-lane predicates.
+__device__ __forceinline__ rsrc_t make_rsrc(const char *base, uint32_t nbytes) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)nbytes, 0x00020000);
+}
+
+// bytes of the first `rows` (<= 64) rows of a [rows, D] slab with row stride `stride` elements;
+// 0 if rows <= 0. The host guarantees 64 * stride * 2 + 256 < 2^31.
+__device__ __forceinline__ uint32_t slab_bytes(int rows, int stride, int D) {
+    return rows <= 0 ? 0u : (uint32_t)(((rows - 1) * stride + D) * 2);
+}
+
+template <class DT, bool kCausal, int kD, bool kExactD>
 __global__ __launch_bounds__(kThreads) void fa_fwd_kernel(const fa_fwd_params p, const int n_qtiles) {
-    __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
+    using G = Geo<kD>;
+    __shared__ __attribute__((aligned(16))) char lds[G::kLdsBytes];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -124,169 +165,188 @@ __global__ __launch_bounds__(kThreads) void fa_fwd_kernel(const fa_fwd_params p,
     // logical order: batch, q-head (members of one kv group adjacent), q-tile
     const uint32_t t = w % (uint32_t)n_qtiles;
     const uint32_t bh = w / (uint32_t)n_qtiles;
-    const int64_t hq = bh % (uint32_t)p.num_heads_q;
-    const int64_t b = bh / (uint32_t)p.num_heads_q;
-    const int64_t qtile = kCausal ? (int64_t)(n_qtiles - 1 - t) : (int64_t)t;  // heavy first
-    const int64_t hkv = hq / p.head_q_per_group;
+    const int hq = (int)(bh % (uint32_t)p.num_heads_q);
+    const int b = (int)(bh / (uint32_t)p.num_heads_q);
+    const int qtile = kCausal ? (n_qtiles - 1 - (int)t) : (int)t;  // heavy tiles first
+    const int hkv = hq / (int)p.head_q_per_group;
 
-    const int64_t Sq = p.seqlen_q, Sk = p.seqlen_kv, D = p.headdim;
+    const int Sq = (int)p.seqlen_q, Sk = (int)p.seqlen_kv, D = (int)p.headdim;
     const float sc = p.softmax_scale;
+    const float thr_raw = kRescaleThr / sc;  // rescale threshold in unscaled score units
 
-    const char *qb = (const char *)p.q_ptr + 2 * (b * p.q_batch_stride + hq * p.q_head_stride);
-    const char *kb = (const char *)p.k_ptr + 2 * (b * p.k_batch_stride + hkv * p.k_head_stride);
-    const char *vb = (const char *)p.v_ptr + 2 * (b * p.v_batch_stride + hkv * p.v_head_stride);
-    char *ob = (char *)p.o_ptr + 2 * (b * p.o_batch_stride + hq * p.o_head_stride);
+    const char *qb = (const char *)p.q_ptr + 2 * ((int64_t)b * p.q_batch_stride + (int64_t)hq * p.q_head_stride);
+    const char *kb = (const char *)p.k_ptr + 2 * ((int64_t)b * p.k_batch_stride + (int64_t)hkv * p.k_head_stride);
+    const char *vb = (const char *)p.v_ptr + 2 * ((int64_t)b * p.v_batch_stride + (int64_t)hkv * p.v_head_stride);
+    char *ob = (char *)p.o_ptr + 2 * ((int64_t)b * p.o_batch_stride + (int64_t)hq * p.o_head_stride);
 
-    const int64_t m0 = qtile * kBlockM;        // first query row of the workgroup
-    const int64_t mw = m0 + wave * 32;         // first query row of this wave
-    const int64_t my_q = mw + r;               // this lane's query row
-    const int64_t diag = Sk - Sq;              // bottom-right causal offset: key n visible iff n <= m + diag
+    const int m0 = qtile * kBlockM;   // first query row of the workgroup
+    const int mw = m0 + wave * 32;    // first query row of this wave
+    const int my_q = mw + r;          // this lane's query row
+    const int diag = Sk - Sq;         // bottom-right causal offset: key n visible iff n <= m + diag
 
     // ---- KV tile range ----------------------------------------------------------------
-    const int64_t n_blocks = (Sk + kBlockN - 1) / kBlockN;
-    int64_t n_end = n_blocks;
+    const int n_blocks = (Sk + kBlockN - 1) / kBlockN;
+    int n_end = n_blocks;
     if (kCausal) {
-        // last valid query of the workgroup sees keys up to (min(m0+BM, Sq) - 1) + diag
-        const int64_t x = diag + (m0 + kBlockM < Sq ? m0 + kBlockM : Sq);
-        const int64_t nb = x <= 0 ? 0 : (x + kBlockN - 1) / kBlockN;
-        n_end = nb < n_blocks ? nb : n_blocks;
+        // the workgroup's last valid query sees keys up to min(m0+BM, Sq) - 1 + diag
+        const int x = diag + min(m0 + kBlockM, Sq);
+        const int nb = x <= 0 ? 0 : (x + kBlockN - 1) / kBlockN;
+        n_end = min(nb, n_blocks);
     }
 
     // ---- Q fragments (B operand of S^T = K.Q^T), resident for the whole loop ----------
-    // lane (h, r) holds Q[my_q][16*ks + 8*h + 0..7] for k-step ks
-    u32x4 qf[8];
+    // lane (h, r) holds Q[my_q][16*ks + 8*h + 0..7] for k-step ks; rows >= Sq read as 0
+    u32x4 qf[G::kKSteps];
     {
-        const bool q_ok = my_q < Sq;
-        const char *qrow = qb + 2 * my_q * p.q_seqlen_stride;
+        const int qs = (int)p.q_seqlen_stride;
+        const rsrc_t qr = make_rsrc(qb + 2 * (int64_t)mw * qs, slab_bytes(min(Sq - mw, 32), qs, D));
+        const int off = r * qs * 2 + 16 * h;
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks) {
-            const int d0 = 16 * ks + 8 * h;
-            qf[ks] = (q_ok && d0 < D) ? *(const u32x4 *)(qrow + 2 * d0) : (u32x4){0, 0, 0, 0};
+        for (int ks = 0; ks < G::kKSteps; ++ks) {
+            qf[ks] = __builtin_amdgcn_raw_buffer_load_b128(qr, off + 32 * ks, 0, 0);
+            if (!kExactD && 16 * ks + 8 * h >= D) qf[ks] = (u32x4){0, 0, 0, 0};
         }
     }
 
     // ---- register staging of K/V tiles ------------------------------------------------
-    // thread t moves 16-B chunk (t & 15) of rows (t >> 4) and (t >> 4) + 32 of both K and V
-    const int srow = tid >> 4;
-    const int sch = tid & 15;
-    const bool sch_ok = sch * 8 < D;
+    // thread t moves 16-B chunk (t % kChunks) of rows t / kChunks (+ 32 for D = 128) of K and V
+    const int srow = tid / G::kChunks;
+    const int sch = tid % G::kChunks;
+    const int ks_ = (int)p.k_seqlen_stride, vs_ = (int)p.v_seqlen_stride;
+    const int koff0 = srow * ks_ * 2 + 16 * sch;
+    const int voff0 = srow * vs_ * 2 + 16 * sch;
+    const int koff1 = koff0 + 32 * ks_ * 2;
+    const int voff1 = voff0 + 32 * vs_ * 2;
+    const bool sch_ok = kExactD || sch * 8 < D;
     u32x4 kst0, kst1, vst0, vst1;
-    const u32x4 zero4 = {0, 0, 0, 0};
 
-    auto stage_load = [&](int64_t j) {
-        const int64_t key0 = j * kBlockN + srow;
-        const int64_t key1 = key0 + 32;
-        const bool ok0 = sch_ok && key0 < Sk;
-        const bool ok1 = sch_ok && key1 < Sk;
-        kst0 = ok0 ? *(const u32x4 *)(kb + 2 * (key0 * p.k_seqlen_stride + sch * 8)) : zero4;
-        kst1 = ok1 ? *(const u32x4 *)(kb + 2 * (key1 * p.k_seqlen_stride + sch * 8)) : zero4;
-        vst0 = ok0 ? *(const u32x4 *)(vb + 2 * (key0 * p.v_seqlen_stride + sch * 8)) : zero4;
-        vst1 = ok1 ? *(const u32x4 *)(vb + 2 * (key1 * p.v_seqlen_stride + sch * 8)) : zero4;
+    auto stage_load = [&](int j) {
+        // descriptors rebased per tile: 32-bit lane offsets stay tile-invariant; rows >= Sk read 0
+        const int key0 = j * kBlockN;
+        const rsrc_t kr = make_rsrc(kb + 2 * (int64_t)key0 * ks_, slab_bytes(min(Sk - key0, kBlockN), ks_, D));
+        const rsrc_t vr = make_rsrc(vb + 2 * (int64_t)key0 * vs_, slab_bytes(min(Sk - key0, kBlockN), vs_, D));
+        kst0 = __builtin_amdgcn_raw_buffer_load_b128(kr, koff0, 0, 0);
+        vst0 = __builtin_amdgcn_raw_buffer_load_b128(vr, voff0, 0, 0);
+        if (G::kStage == 2) {
+            kst1 = __builtin_amdgcn_raw_buffer_load_b128(kr, koff1, 0, 0);
+            vst1 = __builtin_amdgcn_raw_buffer_load_b128(vr, voff1, 0, 0);
+        }
     };
     auto stage_write = [&](int buf) {
-        char *K = lds + buf * kBufBytes;
-        char *V = K + kTileBytes;
-        *(u32x4 *)(K + k_off(srow, sch)) = kst0;
-        *(u32x4 *)(K + k_off(srow + 32, sch)) = kst1;
-        *(u32x4 *)(V + v_off(srow, sch)) = vst0;
-        *(u32x4 *)(V + v_off(srow + 32, sch)) = vst1;
+        char *K = lds + buf * G::kBufBytes;
+        char *V = K + G::kTileBytes;
+        // D < kD: K columns past D must be 0 (they meet Q's zero columns, garbage could be NaN)
+        const u32x4 z = {0, 0, 0, 0};
+        *(u32x4 *)(K + G::k_off(srow, sch)) = sch_ok ? kst0 : z;
+        *(u32x4 *)(V + G::v_off(srow, sch)) = vst0;
+        if (G::kStage == 2) {
+            *(u32x4 *)(K + G::k_off(srow + 32, sch)) = sch_ok ? kst1 : z;
+            *(u32x4 *)(V + G::v_off(srow + 32, sch)) = vst1;
+        }
     };
 
     // ---- per-lane constant LDS addresses ----------------------------------------------
-    // K A-operand: row (kt*32 + r), chunk (2*ks + h)  -> offset k_off(r, 2ks+h) + kt*8192
     // V^T A-operand via ds_read_b64_tr_b16: lane = 16*g + 4*qq + pp supplies row (R + qq),
     // columns dt*32 + 16*(g&1) + 4*pp .. +3 where R = kt*32 + 16*s + 4*(g>>1) (+8 for the
-    // second half of the fragment).
+    // second half of the fragment); it receives column dt*32 + (lane & 31) of rows R..R+3.
     const int g = lane >> 4;
     const int qq = (lane >> 2) & 3;
     const int pp = lane & 3;
-    int v_addr[4];
+    int v_addr[G::kDTiles];
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-        const int row = 4 * (g >> 1) + qq;
-        const int ch = dt * 4 + 2 * (g & 1) + (pp >> 1);
-        v_addr[dt] = v_off(row, ch) + 8 * (pp & 1);
-    }
+    for (int dt = 0; dt < G::kDTiles; ++dt)
+        v_addr[dt] = G::v_off(4 * (g >> 1) + qq, dt * 4 + 2 * (g & 1) + (pp >> 1)) + 8 * (pp & 1);
+    int k_addr[G::kKSteps];
+#pragma unroll
+    for (int ks = 0; ks < G::kKSteps; ++ks) k_addr[ks] = G::k_off(r, 2 * ks + h);
 
-    f32x16 o0 = {}, o1 = {}, o2 = {}, o3 = {};
-    float m_run = -INFINITY;
-    float l_run = 0.f;
+    f32x16 o[G::kDTiles];
+#pragma unroll
+    for (int dt = 0; dt < G::kDTiles; ++dt) o[dt] = (f32x16){};
+    float m_use = kNeg;  // running max used by exp2 (unscaled score units), lags by < kRescaleThr
+    float msc = 0.f;     // m_use * sc, or 0 while the row has seen no visible key
+    float l_run = 0.f;   // lane-partial row sum of P (32 of the 64 keys of each tile)
 
+    if (n_end > 0) stage_load(0);
+    // retire Q and tile 0 here; the asm barrier re-defines qf so the loop's wait analysis does not
+    // see the Q loads as pending (it would otherwise wait vmcnt(0) at the top of every iteration)
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+#pragma unroll
+    for (int ks = 0; ks < G::kKSteps; ++ks) asm volatile("" : "+v"(qf[ks]));
     if (n_end > 0) {
-        stage_load(0);
         stage_write(0);
         if (n_end > 1) stage_load(1);
     }
     __syncthreads();
 
-    for (int64_t j = 0; j < n_end; ++j) {
-        const int buf = (int)(j & 1);
-        const char *K = lds + buf * kBufBytes;
-        const char *V = K + kTileBytes;
-        const int64_t key0 = j * kBlockN;
+    // one KV tile; BUF (the LDS buffer holding tile j) is a compile-time constant so that every
+    // LDS address is a per-lane base plus an immediate offset
+    auto tile = [&](const int j, auto BUF) {
+        constexpr int buf = decltype(BUF)::value;
+        const char *K = lds + buf * G::kBufBytes;
+        const char *V = K + G::kTileBytes;
+        const int key0 = j * kBlockN;
 
         bool wave_active = true;
         bool need_mask = key0 + kBlockN > Sk;
         if (kCausal) {
-            wave_active = key0 <= mw + 31 + diag;           // some key visible to the wave's last row
-            need_mask = need_mask || (key0 + kBlockN - 1 > mw + diag);  // some key hidden from its first row
+            wave_active = key0 <= mw + 31 + diag;                      // a key visible to the last row
+            need_mask = need_mask || (key0 + kBlockN - 1 > mw + diag);  // a key hidden from the first row
         }
 
         if (wave_active) {
-            // ---- S^T = K . Q^T : two 32-key sub-tiles ---------------------------------
+            // ---- S^T = K . Q^T : two 32-key sub-tiles -----------------------------------
             f32x16 s0 = {}, s1 = {};
 #pragma unroll
-            for (int ks = 0; ks < 8; ++ks) {
-                const u32x4 a0 = *(const u32x4 *)(K + k_off(r, 2 * ks + h));
-                const u32x4 a1 = *(const u32x4 *)(K + 8192 + k_off(r, 2 * ks + h));
+            for (int ks = 0; ks < G::kKSteps; ++ks) {
+                const u32x4 a0 = *(const u32x4 *)(K + k_addr[ks]);
+                const u32x4 a1 = *(const u32x4 *)(K + 32 * G::kRowBytes + k_addr[ks]);
                 s0 = DT::mfma(a0, qf[ks], s0);
                 s1 = DT::mfma(a1, qf[ks], s1);
             }
 
-            // ---- mask (only tiles crossing the diagonal or the Sk tail) --------------
+            // ---- mask (only tiles crossing the diagonal or the Sk tail) ----------------
             if (need_mask) {
+                const int lim = kCausal ? min(Sk - 1, my_q + diag) : Sk - 1;  // last visible key
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
-                    const int64_t kk0 = key0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                    const int64_t kk1 = kk0 + 32;
-                    bool m0k = kk0 >= Sk, m1k = kk1 >= Sk;
-                    if (kCausal) {
-                        m0k = m0k || (kk0 > my_q + diag);
-                        m1k = m1k || (kk1 > my_q + diag);
-                    }
-                    if (m0k) s0[i] = -INFINITY;
-                    if (m1k) s1[i] = -INFINITY;
+                    const int kk = key0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    if (kk > lim) s0[i] = kNeg;
+                    if (kk + 32 > lim) s1[i] = kNeg;
                 }
             }
 
-            // ---- online softmax (per lane = per query row) -----------------------------
-            float mx = fmaxf(s0[0], s1[0]);
+            // ---- online softmax (per lane = per query row) -------------------------------
+            float mx = fmaxf(fmaxf(s0[0], s0[1]), fmaxf(s1[0], s1[1]));
 #pragma unroll
-            for (int i = 1; i < 16; ++i) mx = fmaxf(mx, fmaxf(s0[i], s1[i]));
+            for (int i = 2; i < 16; i += 2) mx = fmaxf(mx, fmaxf(fmaxf(s0[i], s0[i + 1]), fmaxf(s1[i], s1[i + 1])));
             mx = pair_max(mx);
-            const float m_new = fmaxf(m_run, mx);
-            const float m_sc = (m_new == -INFINITY) ? 0.f : m_new * sc;
-            const float alpha = __builtin_amdgcn_exp2f(m_run * sc - m_sc);
-            m_run = m_new;
 
-            float ls = 0.f;
+            // deferred rescale: taken by the whole wave when any row's max outgrows m_use
+            float alpha = 1.f;
+            const bool grow = mx > m_use + thr_raw;
+            if (__builtin_amdgcn_ballot_w64(grow)) {
+                const float m_new = fmaxf(m_use, mx);
+                const float msc_new = (m_new <= kNeg) ? 0.f : m_new * sc;
+                alpha = __builtin_amdgcn_exp2f(msc - msc_new);  // msc == 0 && m_use == kNeg: l, O are 0
+                m_use = m_new;
+                msc = msc_new;
+#pragma unroll
+                for (int dt = 0; dt < G::kDTiles; ++dt) o[dt] *= alpha;
+            }
+
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                s0[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s0[i], sc, -m_sc));
-                s1[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s1[i], sc, -m_sc));
-                ls += s0[i] + s1[i];
+                s0[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s0[i], sc, -msc));
+                s1[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s1[i], sc, -msc));
             }
-            l_run = l_run * alpha + ls;
-
-            if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
+            float ls0 = s0[0], ls1 = s1[0];
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    o0[i] *= alpha;
-                    o1[i] *= alpha;
-                    o2[i] *= alpha;
-                    o3[i] *= alpha;
-                }
+            for (int i = 1; i < 16; ++i) {
+                ls0 += s0[i];
+                ls1 += s1[i];
             }
+            l_run = l_run * alpha + (ls0 + ls1);
 
             // ---- P (rounded to T) as the B operand: k-step kk = (kt, s) -> regs 8s..8s+7
             u32x4 pf[4];
@@ -301,50 +361,49 @@ __global__ __launch_bounds__(kThreads) void fa_fwd_kernel(const fa_fwd_params p,
             // ---- O^T += V^T . P^T ------------------------------------------------------
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
-                const int rowoff = (kk >> 1) * 32 * 256 + (kk & 1) * 16 * 256;  // kt*32 + 16*s rows
-                u32x4 a[4];
+                const int rowoff = ((kk >> 1) * 32 + (kk & 1) * 16) * G::kRowBytes;  // kt*32 + 16*s
 #pragma unroll
-                for (int dt = 0; dt < 4; ++dt) {
+                for (int dt = 0; dt < G::kDTiles; ++dt) {
                     const u32x2 lo = tr_read(V + rowoff + v_addr[dt]);
-                    const u32x2 hi = tr_read(V + rowoff + 8 * 256 + v_addr[dt]);
-                    a[dt] = (u32x4){lo[0], lo[1], hi[0], hi[1]};
+                    const u32x2 hi = tr_read(V + rowoff + 8 * G::kRowBytes + v_addr[dt]);
+                    o[dt] = DT::mfma((u32x4){lo[0], lo[1], hi[0], hi[1]}, pf[kk], o[dt]);
                 }
-                o0 = DT::mfma(a[0], pf[kk], o0);
-                o1 = DT::mfma(a[1], pf[kk], o1);
-                o2 = DT::mfma(a[2], pf[kk], o2);
-                o3 = DT::mfma(a[3], pf[kk], o3);
             }
         }
 
         if (j + 1 < n_end) stage_write(buf ^ 1);
         __syncthreads();
         if (j + 2 < n_end) stage_load(j + 2);
+    };
+    for (int j = 0; j < n_end; j += 2) {
+        tile(j, IC<0>{});
+        if (j + 1 < n_end) tile(j + 1, IC<1>{});
     }
 
     // ---- epilogue: O = O^T / l, row per lane, 16-B stores after a half-wave swap ----------
     const float l_tot = pair_sum(l_run);
     const float inv = (l_tot == 0.f) ? 1.f : 1.f / l_tot;
-    const bool q_ok = my_q < Sq;
-    char *orow = ob + 2 * my_q * p.o_seqlen_stride;
-    auto store_tile = [&](const f32x16 &o, int dt) {
+    const int os_ = (int)p.o_seqlen_stride;
+    const rsrc_t orr = make_rsrc(ob + 2 * (int64_t)mw * os_, slab_bytes(min(Sq - mw, 32), os_, D));
+    const int orow = r * os_ * 2;
+#pragma unroll
+    for (int dt = 0; dt < G::kDTiles; ++dt) {
 #pragma unroll
         for (int gp = 0; gp < 4; gp += 2) {
-            // this lane holds d = dt*32 + 8*grp + 4*h + 0..3 in o[4*grp .. 4*grp+3]
-            uint32_t a0 = DT::pack(o[4 * gp + 0] * inv, o[4 * gp + 1] * inv);
-            uint32_t a1 = DT::pack(o[4 * gp + 2] * inv, o[4 * gp + 3] * inv);
-            uint32_t b0 = DT::pack(o[4 * gp + 4] * inv, o[4 * gp + 5] * inv);
-            uint32_t b1 = DT::pack(o[4 * gp + 6] * inv, o[4 * gp + 7] * inv);
-            auto x0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
-            auto x1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+            // this lane holds d = dt*32 + 8*grp + 4*h + 0..3 in o[dt][4*grp .. 4*grp+3]
+            const uint32_t a0 = DT::pack(o[dt][4 * gp + 0] * inv, o[dt][4 * gp + 1] * inv);
+            const uint32_t a1 = DT::pack(o[dt][4 * gp + 2] * inv, o[dt][4 * gp + 3] * inv);
+            const uint32_t b0 = DT::pack(o[dt][4 * gp + 4] * inv, o[dt][4 * gp + 5] * inv);
+            const uint32_t b1 = DT::pack(o[dt][4 * gp + 6] * inv, o[dt][4 * gp + 7] * inv);
+            const auto x0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+            const auto x1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
             // lower half: d = dt*32 + 8*gp + 0..7 ; upper half: d = dt*32 + 8*(gp+1) + 0..7
             const int d0 = dt * 32 + 8 * (gp + h);
-            if (q_ok && d0 < D) *(u32x4 *)(orow + 2 * d0) = (u32x4){x0[0], x1[0], x0[1], x1[1]};
+            if (kExactD || d0 < D)
+                __builtin_amdgcn_raw_buffer_store_b128((u32x4){x0[0], x1[0], x0[1], x1[1]}, orr, orow + 2 * d0, 0,
+                                                       0);
         }
-    };
-    store_tile(o0, 0);
-    store_tile(o1, 1);
-    store_tile(o2, 2);
-    store_tile(o3, 3);
+    }
 }
 
 }  // namespace fa
@@ -392,6 +451,12 @@ int check_params(const fa_fwd_params *p, int dtype, int causal) {
     for (int i = 0; i < 12; ++i)
         if (strides[i] % 8 != 0)
             return set_err(FA_ERR_INVALID_ARGUMENT, "strides must be multiples of 8 elements (16 bytes)");
+    if (p->seqlen_q > 0x3fffffffLL || p->seqlen_kv > 0x3fffffffLL)
+        return set_err(FA_ERR_UNSUPPORTED, "sequence lengths must be < 2^30");
+    // 32-bit lane offsets inside one 64-row K/V tile and one 32-row Q/O slab
+    for (int i = 8; i < 12; ++i)
+        if (strides[i] < 0 || strides[i] * 2 * 64 + 256 > 0x7fffffffLL)
+            return set_err(FA_ERR_UNSUPPORTED, "sequence stride too large for 32-bit tile offsets");
     const int64_t n_qtiles = (p->seqlen_q + fa::kBlockM - 1) / fa::kBlockM;
     const int64_t nwg = n_qtiles * p->num_heads_q * p->batch_size;
     if (nwg > 0x7fffffffLL) return set_err(FA_ERR_UNSUPPORTED, "grid too large (%lld workgroups)", (long long)nwg);
@@ -399,15 +464,24 @@ int check_params(const fa_fwd_params *p, int dtype, int causal) {
     return FA_OK;
 }
 
-template <class DT, bool C>
-int launch(const fa_fwd_params &p, hipStream_t stream) {
+template <class DT, bool C, int kD, bool kExact>
+int launch_one(const fa_fwd_params &p, hipStream_t stream) {
     const int64_t n_qtiles = (p.seqlen_q + fa::kBlockM - 1) / fa::kBlockM;
     const int64_t nwg = n_qtiles * p.num_heads_q * p.batch_size;
-    hipLaunchKernelGGL((fa::fa_fwd_kernel<DT, C>), dim3((uint32_t)nwg), dim3(fa::kThreads), 0, stream, p,
+    hipLaunchKernelGGL((fa::fa_fwd_kernel<DT, C, kD, kExact>), dim3((uint32_t)nwg), dim3(fa::kThreads), 0, stream, p,
                        (int)n_qtiles);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "HIP launch failed: %s", hipGetErrorString(e));
     return FA_OK;
+}
+
+// head-dim dispatch: D <= 64 runs the 64-wide tile, 64 < D <= 128 the 128-wide tile (the reference
+// runs every D <= 128 on its 128 kernel, csrc/kernel_dispatcher.h:45-52)
+template <class DT, bool C>
+int launch(const fa_fwd_params &p, hipStream_t stream) {
+    if (p.headdim <= 64)
+        return p.headdim == 64 ? launch_one<DT, C, 64, true>(p, stream) : launch_one<DT, C, 64, false>(p, stream);
+    return p.headdim == 128 ? launch_one<DT, C, 128, true>(p, stream) : launch_one<DT, C, 128, false>(p, stream);
 }
 
 }  // namespace

@@ -1,3 +1,6 @@
+#!/bin/bash
+# One GPU round: diag -> smoke -> pytest -m gpu -> bench (C2 + other configs). Stops at the first
+# GPU fault / timeout.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
@@ -11,3 +14,6 @@ tail -30 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 echo "== bench"
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 2>&1 | tee gpurun_out/bench_c2.log || exit 1
+for c in ${EXTRA_CONFIGS:-c3 c4 decode}; do
+  timeout -k 10 300 python bench.py --steps 20 --warmup 5 --config $c --no-cpu-baseline 2>&1 | tee gpurun_out/bench_$c.log || exit 1
+done
