@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "fa_gfx950.h"
@@ -65,6 +66,7 @@ struct IC {
 };
 
 struct F16 {
+    static constexpr bool kIsF16 = true;
     static __device__ __forceinline__ f32x16 mfma(u32x4 a, u32x4 b, f32x16 c) {
         return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a),
                                                       __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
@@ -77,6 +79,7 @@ struct F16 {
 };
 
 struct BF16 {
+    static constexpr bool kIsF16 = false;
     static __device__ __forceinline__ f32x16 mfma(u32x4 a, u32x4 b, f32x16 c) {
         return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
                                                        __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
@@ -94,8 +97,9 @@ struct Geo {
     static constexpr int kRowBytes = kD * 2;            // 256 / 128
     static constexpr int kChunks = kD / 8;              // 16-B chunks per row
     static constexpr int kTileBytes = kBlockN * kRowBytes;
-    static constexpr int kBufBytes = 2 * kTileBytes;    // K + V
-    static constexpr int kLdsBytes = 2 * kBufBytes;     // double buffer
+    // LDS ring: 2 K slots + 3 V slots. V needs a third slot because waves 4-7 run their P.V of
+    // tile j after the barrier that publishes tile j+1 (see "stagger" in the kernel).
+    static constexpr int kLdsBytes = 5 * kTileBytes;
     static constexpr int kKSteps = kD / 16;             // k-steps of S^T = K.Q^T
     static constexpr int kDTiles = kD / 32;             // 32-row d tiles of O^T
     static constexpr int kStage = kBlockN * kChunks / kThreads;  // chunks per thread per tile (2 / 1)
@@ -145,7 +149,7 @@ __device__ __forceinline__ uint32_t slab_bytes(int rows, int stride, int D) {
 }
 
 template <class DT, bool kCausal, int kD, bool kExactD>
-__global__ __launch_bounds__(kThreads) void fa_fwd_kernel(const fa_fwd_params p, const int n_qtiles) {
+__global__ __launch_bounds__(kThreads) void fa_fwd_w8(const fa_fwd_params p, const int n_qtiles) {
     using G = Geo<kD>;
     __shared__ __attribute__((aligned(16))) char lds[G::kLdsBytes];
 
@@ -232,9 +236,9 @@ __global__ __launch_bounds__(kThreads) void fa_fwd_kernel(const fa_fwd_params p,
             vst1 = __builtin_amdgcn_raw_buffer_load_b128(vr, voff1, 0, 0);
         }
     };
-    auto stage_write = [&](int buf) {
-        char *K = lds + buf * G::kBufBytes;
-        char *V = K + G::kTileBytes;
+    auto stage_write = [&](int kslot, int vslot) {
+        char *K = lds + kslot * G::kTileBytes;
+        char *V = lds + (2 + vslot) * G::kTileBytes;
         // D < kD: K columns past D must be 0 (they meet Q's zero columns, garbage could be NaN)
         const u32x4 z = {0, 0, 0, 0};
         *(u32x4 *)(K + G::k_off(srow, sch)) = sch_ok ? kst0 : z;
@@ -267,6 +271,88 @@ __global__ __launch_bounds__(kThreads) void fa_fwd_kernel(const fa_fwd_params p,
     float msc = 0.f;     // m_use * sc, or 0 while the row has seen no visible key
     float l_run = 0.f;   // lane-partial row sum of P (32 of the 64 keys of each tile)
 
+    // Stagger (MI355X_MICROARCH "Two waves per SIMD"): waves w and w+4 share a SIMD. Waves 4-7
+    // ("lag") run each tile's P.V after the tile's barrier, i.e. half a tile behind waves 0-3, so
+    // one wave's softmax (VALU) overlaps its partner's MFMAs instead of both waves alternating
+    // between all-MFMA and all-VALU phases in lockstep.
+    const bool lag = wave >= 4;
+    u32x4 pf[4];               // P of the last softmax (B operand of P.V), k-step kk = (kt, s)
+    bool pv_pending = false;   // lag waves: P.V of the previous tile still to do
+    const char *pv_v = lds;    // ... and the V slot it reads
+
+    // S^T = K.Q^T, mask, online softmax; leaves P (rounded to T) in pf
+    auto qk_softmax = [&](const char *K, const int key0, const bool need_mask) {
+        f32x16 s0 = {}, s1 = {};
+#pragma unroll
+        for (int ks = 0; ks < G::kKSteps; ++ks) {
+            const u32x4 a0 = *(const u32x4 *)(K + k_addr[ks]);
+            const u32x4 a1 = *(const u32x4 *)(K + 32 * G::kRowBytes + k_addr[ks]);
+            s0 = DT::mfma(a0, qf[ks], s0);
+            s1 = DT::mfma(a1, qf[ks], s1);
+        }
+        // mask (only tiles crossing the diagonal or the Sk tail)
+        if (need_mask) {
+            const int lim = kCausal ? min(Sk - 1, my_q + diag) : Sk - 1;  // last visible key
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int kk = key0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                if (kk > lim) s0[i] = kNeg;
+                if (kk + 32 > lim) s1[i] = kNeg;
+            }
+        }
+        // online softmax (per lane = per query row)
+        float mx = fmaxf(fmaxf(s0[0], s0[1]), fmaxf(s1[0], s1[1]));
+#pragma unroll
+        for (int i = 2; i < 16; i += 2) mx = fmaxf(mx, fmaxf(fmaxf(s0[i], s0[i + 1]), fmaxf(s1[i], s1[i + 1])));
+        mx = pair_max(mx);
+        // deferred rescale: taken by the whole wave when any row's max outgrows m_use; every
+        // earlier P.V is already in O at this point (lag waves ran theirs first)
+        float alpha = 1.f;
+        const bool grow = mx > m_use + thr_raw;
+        if (__builtin_amdgcn_ballot_w64(grow)) {
+            const float m_new = fmaxf(m_use, mx);
+            const float msc_new = (m_new <= kNeg) ? 0.f : m_new * sc;
+            alpha = __builtin_amdgcn_exp2f(msc - msc_new);  // msc == 0 && m_use == kNeg: l, O are 0
+            m_use = m_new;
+            msc = msc_new;
+#pragma unroll
+            for (int dt = 0; dt < G::kDTiles; ++dt) o[dt] *= alpha;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            s0[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s0[i], sc, -msc));
+            s1[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s1[i], sc, -msc));
+        }
+        float ls0 = s0[0], ls1 = s1[0];
+#pragma unroll
+        for (int i = 1; i < 16; ++i) {
+            ls0 += s0[i];
+            ls1 += s1[i];
+        }
+        l_run = l_run * alpha + (ls0 + ls1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            pf[s] = (u32x4){DT::pack(s0[8 * s + 0], s0[8 * s + 1]), DT::pack(s0[8 * s + 2], s0[8 * s + 3]),
+                            DT::pack(s0[8 * s + 4], s0[8 * s + 5]), DT::pack(s0[8 * s + 6], s0[8 * s + 7])};
+            pf[2 + s] = (u32x4){DT::pack(s1[8 * s + 0], s1[8 * s + 1]), DT::pack(s1[8 * s + 2], s1[8 * s + 3]),
+                                DT::pack(s1[8 * s + 4], s1[8 * s + 5]), DT::pack(s1[8 * s + 6], s1[8 * s + 7])};
+        }
+    };
+
+    // O^T += V^T . P^T
+    auto pv = [&](const char *V) {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const int rowoff = ((kk >> 1) * 32 + (kk & 1) * 16) * G::kRowBytes;  // kt*32 + 16*s
+#pragma unroll
+            for (int dt = 0; dt < G::kDTiles; ++dt) {
+                const u32x2 lo = tr_read(V + rowoff + v_addr[dt]);
+                const u32x2 hi = tr_read(V + rowoff + 8 * G::kRowBytes + v_addr[dt]);
+                o[dt] = DT::mfma((u32x4){lo[0], lo[1], hi[0], hi[1]}, pf[kk], o[dt]);
+            }
+        }
+    };
+
     if (n_end > 0) stage_load(0);
     // retire Q and tile 0 here; the asm barrier re-defines qf so the loop's wait analysis does not
     // see the Q loads as pending (it would otherwise wait vmcnt(0) at the top of every iteration)
@@ -274,17 +360,18 @@ __global__ __launch_bounds__(kThreads) void fa_fwd_kernel(const fa_fwd_params p,
 #pragma unroll
     for (int ks = 0; ks < G::kKSteps; ++ks) asm volatile("" : "+v"(qf[ks]));
     if (n_end > 0) {
-        stage_write(0);
+        stage_write(0, 0);
         if (n_end > 1) stage_load(1);
     }
     __syncthreads();
 
-    // one KV tile; BUF (the LDS buffer holding tile j) is a compile-time constant so that every
-    // LDS address is a per-lane base plus an immediate offset
-    auto tile = [&](const int j, auto BUF) {
-        constexpr int buf = decltype(BUF)::value;
-        const char *K = lds + buf * G::kBufBytes;
-        const char *V = K + G::kTileBytes;
+    // one KV tile; the K slot KB is a compile-time constant (loop unrolled by 2) so K addresses
+    // are a per-lane base plus an immediate offset; the V slot cycles through 3
+    int vslot = 0;
+    auto tile = [&](const int j, auto KB) {
+        constexpr int kslot = decltype(KB)::value;
+        const char *K = lds + kslot * G::kTileBytes;
+        const char *V = lds + (2 + vslot) * G::kTileBytes;
         const int key0 = j * kBlockN;
 
         bool wave_active = true;
@@ -293,85 +380,21 @@ __global__ __launch_bounds__(kThreads) void fa_fwd_kernel(const fa_fwd_params p,
             wave_active = key0 <= mw + 31 + diag;                      // a key visible to the last row
             need_mask = need_mask || (key0 + kBlockN - 1 > mw + diag);  // a key hidden from the first row
         }
-
+        if (pv_pending) {  // lag waves: previous tile's P.V (its V slot is not overwritten until j+2)
+            pv(pv_v);
+            pv_pending = false;
+        }
         if (wave_active) {
-            // ---- S^T = K . Q^T : two 32-key sub-tiles -----------------------------------
-            f32x16 s0 = {}, s1 = {};
-#pragma unroll
-            for (int ks = 0; ks < G::kKSteps; ++ks) {
-                const u32x4 a0 = *(const u32x4 *)(K + k_addr[ks]);
-                const u32x4 a1 = *(const u32x4 *)(K + 32 * G::kRowBytes + k_addr[ks]);
-                s0 = DT::mfma(a0, qf[ks], s0);
-                s1 = DT::mfma(a1, qf[ks], s1);
-            }
-
-            // ---- mask (only tiles crossing the diagonal or the Sk tail) ----------------
-            if (need_mask) {
-                const int lim = kCausal ? min(Sk - 1, my_q + diag) : Sk - 1;  // last visible key
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int kk = key0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                    if (kk > lim) s0[i] = kNeg;
-                    if (kk + 32 > lim) s1[i] = kNeg;
-                }
-            }
-
-            // ---- online softmax (per lane = per query row) -------------------------------
-            float mx = fmaxf(fmaxf(s0[0], s0[1]), fmaxf(s1[0], s1[1]));
-#pragma unroll
-            for (int i = 2; i < 16; i += 2) mx = fmaxf(mx, fmaxf(fmaxf(s0[i], s0[i + 1]), fmaxf(s1[i], s1[i + 1])));
-            mx = pair_max(mx);
-
-            // deferred rescale: taken by the whole wave when any row's max outgrows m_use
-            float alpha = 1.f;
-            const bool grow = mx > m_use + thr_raw;
-            if (__builtin_amdgcn_ballot_w64(grow)) {
-                const float m_new = fmaxf(m_use, mx);
-                const float msc_new = (m_new <= kNeg) ? 0.f : m_new * sc;
-                alpha = __builtin_amdgcn_exp2f(msc - msc_new);  // msc == 0 && m_use == kNeg: l, O are 0
-                m_use = m_new;
-                msc = msc_new;
-#pragma unroll
-                for (int dt = 0; dt < G::kDTiles; ++dt) o[dt] *= alpha;
-            }
-
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                s0[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s0[i], sc, -msc));
-                s1[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s1[i], sc, -msc));
-            }
-            float ls0 = s0[0], ls1 = s1[0];
-#pragma unroll
-            for (int i = 1; i < 16; ++i) {
-                ls0 += s0[i];
-                ls1 += s1[i];
-            }
-            l_run = l_run * alpha + (ls0 + ls1);
-
-            // ---- P (rounded to T) as the B operand: k-step kk = (kt, s) -> regs 8s..8s+7
-            u32x4 pf[4];
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                pf[s] = (u32x4){DT::pack(s0[8 * s + 0], s0[8 * s + 1]), DT::pack(s0[8 * s + 2], s0[8 * s + 3]),
-                                DT::pack(s0[8 * s + 4], s0[8 * s + 5]), DT::pack(s0[8 * s + 6], s0[8 * s + 7])};
-                pf[2 + s] = (u32x4){DT::pack(s1[8 * s + 0], s1[8 * s + 1]), DT::pack(s1[8 * s + 2], s1[8 * s + 3]),
-                                    DT::pack(s1[8 * s + 4], s1[8 * s + 5]), DT::pack(s1[8 * s + 6], s1[8 * s + 7])};
-            }
-
-            // ---- O^T += V^T . P^T ------------------------------------------------------
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) {
-                const int rowoff = ((kk >> 1) * 32 + (kk & 1) * 16) * G::kRowBytes;  // kt*32 + 16*s
-#pragma unroll
-                for (int dt = 0; dt < G::kDTiles; ++dt) {
-                    const u32x2 lo = tr_read(V + rowoff + v_addr[dt]);
-                    const u32x2 hi = tr_read(V + rowoff + 8 * G::kRowBytes + v_addr[dt]);
-                    o[dt] = DT::mfma((u32x4){lo[0], lo[1], hi[0], hi[1]}, pf[kk], o[dt]);
-                }
+            qk_softmax(K, key0, need_mask);
+            if (lag) {
+                pv_pending = true;
+                pv_v = V;
+            } else {
+                pv(V);
             }
         }
-
-        if (j + 1 < n_end) stage_write(buf ^ 1);
+        vslot = vslot == 2 ? 0 : vslot + 1;
+        if (j + 1 < n_end) stage_write(kslot ^ 1, vslot);
         __syncthreads();
         if (j + 2 < n_end) stage_load(j + 2);
     };
@@ -379,6 +402,7 @@ __global__ __launch_bounds__(kThreads) void fa_fwd_kernel(const fa_fwd_params p,
         tile(j, IC<0>{});
         if (j + 1 < n_end) tile(j + 1, IC<1>{});
     }
+    if (pv_pending) pv(pv_v);
 
     // ---- epilogue: O = O^T / l, row per lane, 16-B stores after a half-wave swap ----------
     const float l_tot = pair_sum(l_run);
@@ -404,6 +428,506 @@ __global__ __launch_bounds__(kThreads) void fa_fwd_kernel(const fa_fwd_params p,
                                                        0);
         }
     }
+}
+
+
+// =============================================================================================
+// fa_fwd_w4: one wave per SIMD, 64 query rows per wave (two 32-row blocks A and B), software
+// pipelined so that every MFMA stretch of one block runs beside the softmax VALU of the other:
+//
+//   phase 1: S_A(j)  = K_j . Q_A^T        ||  softmax part 2 of B (tile j-1)
+//   phase 2: O_B    += V_{j-1}^T . P_B^T  ||  softmax part 1 of A (tile j)   -> rescale O_A
+//   phase 3: S_B(j)  = K_j . Q_B^T        ||  softmax part 2 of A (tile j)
+//   phase 4: O_A    += V_j^T . P_A^T      ||  softmax part 1 of B (tile j)   -> rescale O_B
+//
+// Within a phase the MFMAs (inline asm, 2 or 4 per group) and slices of the other block's softmax
+// alternate in program order, pinned by sched_barrier; operand fragments are read from LDS one
+// group ahead. The O accumulators of both blocks live in AGPRs for the whole kernel (asm "+a"
+// operands); S, P, Q/K/V fragments and the softmax state stay in the 256 arch VGPRs.
+// K/V tiles arrive by LDS-DMA (buffer_load ... lds, 1 KiB per wave-instruction) issued one tile
+// ahead into a 2-slot K / 3-slot V ring; the XOR swizzle of the LDS images is applied on the
+// per-lane SOURCE offsets (the DMA destination is lane-linear). Q is DMA'd to LDS once and its
+// fragments are re-read per tile. One barrier per tile.
+// Tiles that need masking (causal diagonal, Sk tail) or where a block is idle run a plain,
+// non-pipelined body after the pipeline has been drained.
+// =============================================================================================
+
+// S += A.B for the two 32-key sub-tiles (same Q fragment); kFirst: C = 0.
+template <bool kF16, bool kFirst>
+__device__ __forceinline__ void mfma_s(f32x16 &s0, f32x16 &s1, const u32x4 &a0, const u32x4 &a1, const u32x4 &q) {
+    if constexpr (kFirst) {
+        if constexpr (kF16)
+            asm volatile("v_mfma_f32_32x32x16_f16 %0, %2, %4, 0\n\tv_mfma_f32_32x32x16_f16 %1, %3, %4, 0"
+                         : "=&v"(s0), "=&v"(s1) : "v"(a0), "v"(a1), "v"(q));
+        else
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %2, %4, 0\n\tv_mfma_f32_32x32x16_bf16 %1, %3, %4, 0"
+                         : "=&v"(s0), "=&v"(s1) : "v"(a0), "v"(a1), "v"(q));
+    } else {
+        if constexpr (kF16)
+            asm volatile("v_mfma_f32_32x32x16_f16 %0, %2, %4, %0\n\tv_mfma_f32_32x32x16_f16 %1, %3, %4, %1"
+                         : "+v"(s0), "+v"(s1) : "v"(a0), "v"(a1), "v"(q));
+        else
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %2, %4, %0\n\tv_mfma_f32_32x32x16_bf16 %1, %3, %4, %1"
+                         : "+v"(s0), "+v"(s1) : "v"(a0), "v"(a1), "v"(q));
+    }
+}
+
+#include "fa_agpr_asm.inc"
+
+// O^T[dt] += V^T[dt] . P^T for the d-tiles of the block whose accumulators start at a[BASE]
+template <bool kF16, int DTL, int BASE>
+__device__ __forceinline__ void agpr_pv(const u32x4 *va, const u32x4 &pf) {
+    if constexpr (kF16) {
+        if constexpr (DTL == 4) {
+            if constexpr (BASE == 0) fa_agpr_pv_f16_4_0(va, pf); else fa_agpr_pv_f16_4_64(va, pf);
+        } else {
+            if constexpr (BASE == 0) fa_agpr_pv_f16_2_0(va, pf); else fa_agpr_pv_f16_2_32(va, pf);
+        }
+    } else {
+        if constexpr (DTL == 4) {
+            if constexpr (BASE == 0) fa_agpr_pv_bf16_4_0(va, pf); else fa_agpr_pv_bf16_4_64(va, pf);
+        } else {
+            if constexpr (BASE == 0) fa_agpr_pv_bf16_2_0(va, pf); else fa_agpr_pv_bf16_2_32(va, pf);
+        }
+    }
+}
+template <int DTL, int BASE>
+__device__ __forceinline__ void agpr_scale(const float alpha) {
+    if constexpr (DTL == 4) {
+        if constexpr (BASE == 0) fa_agpr_scale_4_0(alpha); else fa_agpr_scale_4_64(alpha);
+    } else {
+        if constexpr (BASE == 0) fa_agpr_scale_2_0(alpha); else fa_agpr_scale_2_32(alpha);
+    }
+}
+template <int BASE>
+__device__ __forceinline__ f32x16 agpr_read16() {
+    float x[16];
+    if constexpr (BASE == 0) fa_agpr_read16_0(x);
+    else if constexpr (BASE == 16) fa_agpr_read16_16(x);
+    else if constexpr (BASE == 32) fa_agpr_read16_32(x);
+    else if constexpr (BASE == 48) fa_agpr_read16_48(x);
+    else if constexpr (BASE == 64) fa_agpr_read16_64(x);
+    else if constexpr (BASE == 80) fa_agpr_read16_80(x);
+    else if constexpr (BASE == 96) fa_agpr_read16_96(x);
+    else fa_agpr_read16_112(x);
+    f32x16 v;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = x[i];
+    return v;
+}
+
+// An asm-issued MFMA's result is invisible to hipcc's hazard recognizer: before the first VALU
+// read of S (or AGPR read of O) after its last MFMA, 21 wait states (32x32x16 = 16 passes).
+__device__ __forceinline__ void s_ready(f32x16 &s0, f32x16 &s1) {
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" : "+v"(s0), "+v"(s1));
+}
+__device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" ::: "memory"); }
+
+#define FA_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+
+// Opaque redefinition: ties a value to this point of the (volatile-asm ordered) instruction stream,
+// so IR-level sinking / hoisting cannot move the VALU slices out of their MFMA gap.
+__device__ __forceinline__ void pin(float &x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(u32x4 &x) { asm volatile("" : "+v"(x)); }
+
+__device__ __forceinline__ uint32_t lds_u32(const void *ptr) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)ptr;
+}
+
+// LDS-DMA of NP 1-KiB pieces (one per wave-instruction) from rs + voff[n] to LDS lds0 + n*1024.
+// Issued from asm so hipcc does not see an LDS write it cannot disambiguate (it would otherwise
+// wait vmcnt(0) before the next ds_read of any slot); the caller retires it with an explicit
+// s_waitcnt vmcnt(0) before the tile's barrier. M0 is saved and restored around the statement.
+template <int NP>
+__device__ __forceinline__ void dma_pieces(const rsrc_t &rs, const uint32_t lds0, const int *voff) {
+    uint32_t keep;
+    if constexpr (NP == 4)
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_nop 4\n\t"
+            "s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %6, 0 offen lds\n\t"
+            "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %3, %6, 0 offen lds\n\t"
+            "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %4, %6, 0 offen lds\n\t"
+            "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %5, %6, 0 offen lds\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "s"(lds0), "v"(voff[0]), "v"(voff[1]), "v"(voff[2]), "v"(voff[3]), "s"(rs)
+            : "memory");
+    else
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_nop 4\n\t"
+            "s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %4, 0 offen lds\n\t"
+            "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %3, %4, 0 offen lds\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "s"(lds0), "v"(voff[0]), "v"(voff[1]), "s"(rs)
+            : "memory");
+}
+__device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+template <class DT, bool kCausal, int kD, bool kExactD>
+__global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const int n_qtiles) {
+    using G = Geo<kD>;
+    constexpr bool F = DT::kIsF16;
+    constexpr int KS = G::kKSteps;
+    constexpr int DTL = G::kDTiles;
+    constexpr int RB = G::kRowBytes;
+    constexpr int NP = G::kTileBytes / 4 / 1024;  // LDS-DMA pieces per wave per K or V tile (4 / 2)
+    constexpr int ROWS_PER_PIECE = 1024 / RB;
+    // LDS: Q of the 4 waves (64 rows each) | K slots 0,1 | V slots 0,1,2
+    constexpr int QB = 4 * G::kTileBytes;
+    __shared__ __attribute__((aligned(1024))) char lds[QB + 5 * G::kTileBytes];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31;
+    const int h = lane >> 5;
+
+    // ---- XCD-aware work decode (as fa_fwd_w8) ------------------------------------------
+    const uint32_t nwg = gridDim.x;
+    const uint32_t bid = blockIdx.x;
+    const uint32_t xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const uint32_t w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const uint32_t t = w % (uint32_t)n_qtiles;
+    const uint32_t bh = w / (uint32_t)n_qtiles;
+    const int hq = (int)(bh % (uint32_t)p.num_heads_q);
+    const int b = (int)(bh / (uint32_t)p.num_heads_q);
+    const int qtile = kCausal ? (n_qtiles - 1 - (int)t) : (int)t;
+    const int hkv = hq / (int)p.head_q_per_group;
+
+    const int Sq = (int)p.seqlen_q, Sk = (int)p.seqlen_kv, D = (int)p.headdim;
+    const float sc = p.softmax_scale;
+    const float thr_raw = kRescaleThr / sc;
+
+    const char *qb = (const char *)p.q_ptr + 2 * ((int64_t)b * p.q_batch_stride + (int64_t)hq * p.q_head_stride);
+    const char *kb = (const char *)p.k_ptr + 2 * ((int64_t)b * p.k_batch_stride + (int64_t)hkv * p.k_head_stride);
+    const char *vb = (const char *)p.v_ptr + 2 * ((int64_t)b * p.v_batch_stride + (int64_t)hkv * p.v_head_stride);
+    char *ob = (char *)p.o_ptr + 2 * ((int64_t)b * p.o_batch_stride + (int64_t)hq * p.o_head_stride);
+
+    const int m0 = qtile * kBlockM;
+    const int mw = m0 + wave * 64;  // block A: rows mw..mw+31, block B: rows mw+32..mw+63
+    const int diag = Sk - Sq;
+
+    const int n_blocks = (Sk + kBlockN - 1) / kBlockN;
+    int n_end = n_blocks;
+    if (kCausal) {
+        const int x = diag + min(m0 + kBlockM, Sq);
+        const int nb = x <= 0 ? 0 : (x + kBlockN - 1) / kBlockN;
+        n_end = min(nb, n_blocks);
+    }
+    // leading tiles with no masked score for any row of this wave (pipelined body)
+    int n_pipe = Sk / kBlockN;
+    if (kCausal) {
+        const int x = mw + diag + 1;  // keys visible to the wave's first row
+        n_pipe = min(n_pipe, x <= 0 ? 0 : x / kBlockN);
+    }
+    n_pipe = min(n_pipe, n_end);
+
+    // ---- Q: this wave's 64 rows go to LDS once (LDS-DMA, K-style swizzle on the source side) --
+    const int qs = (int)p.q_seqlen_stride;
+    char *const Qw = lds + wave * G::kTileBytes;
+    typedef __attribute__((address_space(3))) void lds_void;
+    {
+        const rsrc_t qr = make_rsrc(qb + 2 * (int64_t)mw * qs, slab_bytes(min(Sq - mw, 64), qs, D));
+        int qoff[4 * NP];
+#pragma unroll
+        for (int n = 0; n < 4 * NP; ++n) {
+            const int row = n * ROWS_PER_PIECE + (16 * lane) / RB;
+            const int slot = ((16 * lane) % RB) / 16;
+            const int ch = G::k_off(row, slot) % RB / 16;
+            qoff[n] = (kExactD || ch * 8 < D) ? row * qs * 2 + 16 * ch : 0x7ffffff0;  // past the end -> 0
+        }
+#pragma unroll
+        for (int n = 0; n < 4; ++n) dma_pieces<NP>(qr, lds_u32(Qw) + n * NP * 1024, qoff + n * NP);
+    }
+
+    // ---- LDS-DMA staging: this wave writes pieces (wave*NP + n) of each K and V tile --------
+    const int ks_ = (int)p.k_seqlen_stride, vs_ = (int)p.v_seqlen_stride;
+    int kvo[NP], vvo[NP];
+#pragma unroll
+    for (int n = 0; n < NP; ++n) {
+        const int row = (wave * NP + n) * ROWS_PER_PIECE + (16 * lane) / RB;
+        const int slot = ((16 * lane) % RB) / 16;
+        const int kch = G::k_off(row, slot) % RB / 16;  // the XOR swizzles are involutions
+        const int vch = G::v_off(row, slot) % RB / 16;
+        kvo[n] = (kExactD || kch * 8 < D) ? row * ks_ * 2 + 16 * kch : 0x7ffffff0;
+        vvo[n] = (kExactD || vch * 8 < D) ? row * vs_ * 2 + 16 * vch : 0x7ffffff0;
+    }
+    auto stage = [&](const int j, const int kslot, const int vslot) {
+        const int key0 = j * kBlockN;
+        const int rows = min(Sk - key0, kBlockN);
+        const rsrc_t kr = make_rsrc(kb + 2 * (int64_t)key0 * ks_, slab_bytes(rows, ks_, D));
+        const rsrc_t vr = make_rsrc(vb + 2 * (int64_t)key0 * vs_, slab_bytes(rows, vs_, D));
+        dma_pieces<NP>(kr, lds_u32(lds + QB + kslot * G::kTileBytes) + wave * NP * 1024, kvo);
+        dma_pieces<NP>(vr, lds_u32(lds + QB + (2 + vslot) * G::kTileBytes) + wave * NP * 1024, vvo);
+    };
+
+    // ---- per-lane LDS read addresses -----------------------------------------------------
+    const int g = lane >> 4;
+    const int qq = (lane >> 2) & 3;
+    const int pp = lane & 3;
+    int v_addr[DTL];
+#pragma unroll
+    for (int dt = 0; dt < DTL; ++dt)
+        v_addr[dt] = G::v_off(4 * (g >> 1) + qq, dt * 4 + 2 * (g & 1) + (pp >> 1)) + 8 * (pp & 1);
+    int k_addr[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) k_addr[ks] = G::k_off(r, 2 * ks + h);
+
+    // ---- per-block state -----------------------------------------------------------------
+    // O^T of block A lives in a[0 : 16*DTL), of block B in a[16*DTL : 32*DTL) (fa_agpr_asm.inc)
+    constexpr int BASE_A = 0, BASE_B = 16 * DTL;
+    struct Blk {
+        f32x16 s0, s1;   // S^T of the current tile (keys 0-31 / 32-63)
+        u32x4 pf[4];     // P rounded to T, B operand of P.V (k-step kk = (kt, s))
+        float m, msc, l, alpha, ls;
+        bool resc;
+    };
+    Blk A, B;
+    if constexpr (DTL == 4) fa_agpr_zero_128(); else fa_agpr_zero_64();
+    A.m = B.m = kNeg;
+    A.msc = B.msc = 0.f;
+    A.l = B.l = 0.f;
+    A.alpha = B.alpha = 1.f;
+    A.resc = B.resc = false;
+
+    // S^T of one block: fragment reads one k-step ahead of the MFMAs; `slice(ks)` is VALU work of
+    // the other block placed after k-step ks's MFMA pair
+    auto qk = [&](const char *K, const char *Qb, Blk &X, auto &&slice) {
+        u32x4 a0[2], a1[2], qv[2];
+        a0[0] = *(const u32x4 *)(K + k_addr[0]);
+        a1[0] = *(const u32x4 *)(K + 32 * RB + k_addr[0]);
+        qv[0] = *(const u32x4 *)(Qb + k_addr[0]);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int c = ks & 1, nx = c ^ 1;
+            if (ks + 1 < KS) {
+                a0[nx] = *(const u32x4 *)(K + k_addr[ks + 1]);
+                a1[nx] = *(const u32x4 *)(K + 32 * RB + k_addr[ks + 1]);
+                qv[nx] = *(const u32x4 *)(Qb + k_addr[ks + 1]);
+            }
+            if (ks == 0)
+                mfma_s<F, true>(X.s0, X.s1, a0[c], a1[c], qv[c]);
+            else
+                mfma_s<F, false>(X.s0, X.s1, a0[c], a1[c], qv[c]);
+            slice(ks);
+            FA_SCHED_FENCE();
+        }
+    };
+    // O^T += V^T.P^T of one block: 4 groups of DTL MFMAs, V fragments one group ahead;
+    // `slice(kk)` is VALU work of the other block placed after group kk
+    auto pv = [&](const char *V, Blk &X, auto BASE, auto &&slice) {
+        u32x4 va[2][DTL];
+        auto rd = [&](int kk, u32x4 *dst) {
+            const int rowoff = ((kk >> 1) * 32 + (kk & 1) * 16) * RB;
+#pragma unroll
+            for (int dt = 0; dt < DTL; ++dt) {
+                const u32x2 lo = tr_read(V + rowoff + v_addr[dt]);
+                const u32x2 hi = tr_read(V + rowoff + 8 * RB + v_addr[dt]);
+                dst[dt] = (u32x4){lo[0], lo[1], hi[0], hi[1]};
+            }
+        };
+        rd(0, va[0]);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            if (kk + 1 < 4) rd(kk + 1, va[(kk + 1) & 1]);
+            agpr_pv<F, DTL, decltype(BASE)::value>(va[kk & 1], X.pf[kk]);
+            slice(kk);
+            FA_SCHED_FENCE();
+        }
+    };
+
+    // softmax part 1 (4 slices): row max, deferred-rescale decision, P of keys 0-31
+    auto sm1 = [&](Blk &X, const int part) {
+        if (part == 0) {
+            s_ready(X.s0, X.s1);
+            pin(X.ls);
+            float m0_ = fmaxf(fmaxf(X.s0[0], X.s0[1]), fmaxf(X.s1[0], X.s1[1]));
+#pragma unroll
+            for (int i = 2; i < 8; i += 2) m0_ = fmaxf(m0_, fmaxf(fmaxf(X.s0[i], X.s0[i + 1]), fmaxf(X.s1[i], X.s1[i + 1])));
+            X.ls = m0_;  // partial max parked in ls
+            pin(X.ls);
+        } else if (part == 1) {
+            pin(X.ls);
+            float mx = X.ls;
+#pragma unroll
+            for (int i = 8; i < 16; i += 2) mx = fmaxf(mx, fmaxf(fmaxf(X.s0[i], X.s0[i + 1]), fmaxf(X.s1[i], X.s1[i + 1])));
+            mx = pair_max(mx);
+            X.resc = __builtin_amdgcn_ballot_w64(mx > X.m + thr_raw) != 0;
+            const float m_new = X.resc ? fmaxf(X.m, mx) : X.m;
+            const float msc_new = X.resc ? ((m_new <= kNeg) ? 0.f : m_new * sc) : X.msc;
+            X.alpha = __builtin_amdgcn_exp2f(X.msc - msc_new);
+            X.m = m_new;
+            X.msc = msc_new;
+            pin(X.msc);
+            pin(X.alpha);
+        } else {
+            const int i0 = (part - 2) * 8;  // keys i0..i0+7 of sub-tile 0 -> pf[(part-2)]
+            pin(X.msc);
+#pragma unroll
+            for (int i = i0; i < i0 + 8; ++i) X.s0[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(X.s0[i], sc, -X.msc));
+            float ls = X.s0[i0];
+#pragma unroll
+            for (int i = i0 + 1; i < i0 + 8; ++i) ls += X.s0[i];
+            X.pf[part - 2] = (u32x4){DT::pack(X.s0[i0 + 0], X.s0[i0 + 1]), DT::pack(X.s0[i0 + 2], X.s0[i0 + 3]),
+                                     DT::pack(X.s0[i0 + 4], X.s0[i0 + 5]), DT::pack(X.s0[i0 + 6], X.s0[i0 + 7])};
+            pin(X.pf[part - 2]);
+            if (part == 2) {
+                X.ls = ls;
+                pin(X.ls);
+            } else {
+                X.l = X.l * X.alpha + (X.ls + ls);
+                pin(X.l);
+            }
+        }
+    };
+    // softmax part 2 (KS slices): P of keys 32-63
+    auto sm2 = [&](Blk &X, const int part) {
+        constexpr int per = 16 / KS;  // values per slice (2 for D=128, 4 for D=64)
+        const int i0 = part * per;
+        pin(X.msc);
+#pragma unroll
+        for (int i = i0; i < i0 + per; ++i) X.s1[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(X.s1[i], sc, -X.msc));
+        float ls = X.s1[i0];
+#pragma unroll
+        for (int i = i0 + 1; i < i0 + per; ++i) ls += X.s1[i];
+        X.ls = (part == 0) ? ls : X.ls + ls;
+        pin(X.ls);
+        if ((i0 + per) % 8 == 0) {
+            const int q0 = i0 + per - 8;
+            X.pf[2 + q0 / 8] = (u32x4){DT::pack(X.s1[q0 + 0], X.s1[q0 + 1]), DT::pack(X.s1[q0 + 2], X.s1[q0 + 3]),
+                                       DT::pack(X.s1[q0 + 4], X.s1[q0 + 5]), DT::pack(X.s1[q0 + 6], X.s1[q0 + 7])};
+            pin(X.pf[2 + q0 / 8]);
+        }
+        if (part == KS - 1) {
+            X.l += X.ls;
+            pin(X.l);
+        }
+    };
+    // rare path: O *= alpha in place in the AGPRs
+    auto rescale = [&](Blk &X, auto BASE) { agpr_scale<DTL, decltype(BASE)::value>(X.alpha); };
+    auto mask = [&](Blk &X, const int key0, const int row) {
+        const int lim = kCausal ? min(Sk - 1, row + diag) : Sk - 1;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int kk = key0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+            if (kk > lim) X.s0[i] = kNeg;
+            if (kk + 32 > lim) X.s1[i] = kNeg;
+        }
+    };
+    auto none = [](int) {};
+
+    // ---- prologue -------------------------------------------------------------------------
+    // B's "previous tile" in the first pipelined iteration is empty: S = kNeg gives P = 0, and its
+    // P.V reads V slot 2, zeroed here so that 0 * V stays 0.
+#pragma unroll
+    for (int i = 0; i < 16; ++i) B.s1[i] = kNeg;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) B.pf[kk] = (u32x4){0, 0, 0, 0};
+    B.ls = 0.f;
+    {
+        constexpr int per_thread = G::kTileBytes / 256 / 16;
+#pragma unroll
+        for (int i = 0; i < per_thread; ++i)
+            *(u32x4 *)(lds + QB + 4 * G::kTileBytes + (i * 256 + tid) * 16) = (u32x4){0, 0, 0, 0};
+    }
+    if (n_end > 0) stage(0, 0, 0);
+    dma_wait();       // Q and tile 0 landed
+    __syncthreads();  // tile 0 and the zero slot visible to every wave
+    const char *const QA = Qw;
+    const char *const QBk = Qw + 32 * RB;
+
+    // ---- pipelined tiles -----------------------------------------------------------------
+    int vprev = 2;  // V slot of tile j-1 (the zeroed slot before the first tile)
+    int j = 0;
+    for (; j < n_pipe; ++j) {
+        const int kslot = j & 1;
+        const int vcur = vprev == 2 ? 0 : vprev + 1;
+        const int vnext = vcur == 2 ? 0 : vcur + 1;
+        if (j + 1 < n_end) stage(j + 1, kslot ^ 1, vnext);
+        const char *K = lds + QB + kslot * G::kTileBytes;
+        const char *Vp = lds + QB + (2 + vprev) * G::kTileBytes;
+        const char *Vc = lds + QB + (2 + vcur) * G::kTileBytes;
+
+        qk(K, QA, A, [&](int ks) { sm2(B, ks); });           // phase 1
+        pv(Vp, B, IC<BASE_B>{}, [&](int kk) { sm1(A, kk); });   // phase 2
+        if (A.resc) rescale(A, IC<BASE_A>{});
+        qk(K, QBk, B, [&](int ks) { sm2(A, ks); });          // phase 3
+        pv(Vc, A, IC<BASE_A>{}, [&](int kk) { sm1(B, kk); });   // phase 4
+        if (B.resc) rescale(B, IC<BASE_B>{});
+
+        dma_wait();       // tile j+1 landed
+        __syncthreads();
+        vprev = vcur;
+    }
+    if (n_pipe > 0) {  // drain: B's softmax part 2 and P.V of the last pipelined tile
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) sm2(B, ks);
+        pv(lds + QB + (2 + vprev) * G::kTileBytes, B, IC<BASE_B>{}, none);
+    }
+
+    // ---- remaining tiles: masked and/or partially idle, not pipelined ---------------------
+    for (; j < n_end; ++j) {
+        const int kslot = j & 1;
+        const int vcur = vprev == 2 ? 0 : vprev + 1;
+        const int vnext = vcur == 2 ? 0 : vcur + 1;
+        if (j + 1 < n_end) stage(j + 1, kslot ^ 1, vnext);
+        const char *K = lds + QB + kslot * G::kTileBytes;
+        const char *Vc = lds + QB + (2 + vcur) * G::kTileBytes;
+        const int key0 = j * kBlockN;
+        auto full = [&](Blk &X, const char *Qx, const int row, auto BASE) {
+            qk(K, Qx, X, none);
+            s_ready(X.s0, X.s1);
+            mask(X, key0, row);
+#pragma unroll
+            for (int part = 0; part < 4; ++part) sm1(X, part);
+            if (X.resc) rescale(X, BASE);
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) sm2(X, ks);
+            pv(Vc, X, BASE, none);
+        };
+        if (!kCausal || key0 <= mw + 31 + diag) full(A, QA, mw + r, IC<BASE_A>{});
+        if (!kCausal || key0 <= mw + 63 + diag) full(B, QBk, mw + 32 + r, IC<BASE_B>{});
+        dma_wait();
+        __syncthreads();
+        vprev = vcur;
+    }
+
+    // ---- epilogue ---------------------------------------------------------------------------
+    mfma_drain();  // last asm MFMA -> AGPR reads
+    const int os_ = (int)p.o_seqlen_stride;
+    const rsrc_t orr = make_rsrc(ob + 2 * (int64_t)mw * os_, slab_bytes(min(Sq - mw, 64), os_, D));
+    auto store_block = [&](const Blk &X, const int row, auto BASE) {
+        constexpr int base = decltype(BASE)::value;
+        f32x16 o[DTL];
+        o[0] = agpr_read16<base>();
+        o[1] = agpr_read16<base + 16>();
+        if constexpr (DTL == 4) {
+            o[2] = agpr_read16<base + 32>();
+            o[3] = agpr_read16<base + 48>();
+        }
+        const float l_tot = pair_sum(X.l);
+        const float inv = (l_tot == 0.f) ? 1.f : 1.f / l_tot;
+        const int orow = row * os_ * 2;
+#pragma unroll
+        for (int dt = 0; dt < DTL; ++dt) {
+#pragma unroll
+            for (int gp = 0; gp < 4; gp += 2) {
+                const uint32_t a0 = DT::pack(o[dt][4 * gp + 0] * inv, o[dt][4 * gp + 1] * inv);
+                const uint32_t a1 = DT::pack(o[dt][4 * gp + 2] * inv, o[dt][4 * gp + 3] * inv);
+                const uint32_t b0 = DT::pack(o[dt][4 * gp + 4] * inv, o[dt][4 * gp + 5] * inv);
+                const uint32_t b1 = DT::pack(o[dt][4 * gp + 6] * inv, o[dt][4 * gp + 7] * inv);
+                const auto x0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+                const auto x1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+                const int d0 = dt * 32 + 8 * (gp + h);
+                if (kExactD || d0 < D)
+                    __builtin_amdgcn_raw_buffer_store_b128((u32x4){x0[0], x1[0], x0[1], x1[1]}, orr, orow + 2 * d0, 0,
+                                                           0);
+            }
+        }
+    };
+    store_block(A, r, IC<BASE_A>{});
+    store_block(B, r + 32, IC<BASE_B>{});
 }
 
 }  // namespace fa
@@ -464,12 +988,23 @@ int check_params(const fa_fwd_params *p, int dtype, int causal) {
     return FA_OK;
 }
 
+// Kernel variant: 0 = fa_fwd_w4 (default), 1 = fa_fwd_w8. FA_GFX950_VARIANT=w8 selects the
+// 8-wave register-staged kernel (kept for A/B measurements and as a cross-check in the tests).
+int variant_from_env() {
+    const char *v = getenv("FA_GFX950_VARIANT");
+    return (v && strcmp(v, "w8") == 0) ? 1 : 0;
+}
+
 template <class DT, bool C, int kD, bool kExact>
 int launch_one(const fa_fwd_params &p, hipStream_t stream) {
     const int64_t n_qtiles = (p.seqlen_q + fa::kBlockM - 1) / fa::kBlockM;
     const int64_t nwg = n_qtiles * p.num_heads_q * p.batch_size;
-    hipLaunchKernelGGL((fa::fa_fwd_kernel<DT, C, kD, kExact>), dim3((uint32_t)nwg), dim3(fa::kThreads), 0, stream, p,
-                       (int)n_qtiles);
+    if (variant_from_env() == 1)
+        hipLaunchKernelGGL((fa::fa_fwd_w8<DT, C, kD, kExact>), dim3((uint32_t)nwg), dim3(fa::kThreads), 0, stream, p,
+                           (int)n_qtiles);
+    else
+        hipLaunchKernelGGL((fa::fa_fwd_w4<DT, C, kD, kExact>), dim3((uint32_t)nwg), dim3(256), 0, stream, p,
+                           (int)n_qtiles);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "HIP launch failed: %s", hipGetErrorString(e));
     return FA_OK;

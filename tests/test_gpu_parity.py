@@ -29,8 +29,12 @@ pytestmark = pytest.mark.gpu
 TOL = {torch.float16: (2e-3, 2e-3, 1e-4), torch.bfloat16: (1.6e-2, 1.6e-2, 1e-3)}
 
 
-@pytest.fixture(scope="module")
-def fa(device):
+@pytest.fixture(scope="module", params=["w4", "w8"])
+def fa(device, request):
+    # both kernel variants (include/fa_gfx950.h; FA_GFX950_VARIANT selects at launch time)
+    import os
+
+    os.environ["FA_GFX950_VARIANT"] = request.param
     import flash_attention_cute_amd as m
     from flash_attention_cute_amd import flash_attention as fam
 
