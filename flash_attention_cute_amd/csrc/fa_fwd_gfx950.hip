@@ -474,29 +474,21 @@ __device__ __forceinline__ void mfma_s(f32x16 &s0, f32x16 &s1, const u32x4 &a0, 
 
 #include "fa_agpr_asm.inc"
 
-// O^T[dt] += V^T[dt] . P^T for the d-tiles of the block whose accumulators start at a[BASE]
-template <bool kF16, int DTL, int BASE>
-__device__ __forceinline__ void agpr_pv(const u32x4 *va, const u32x4 &pf) {
+// one 16-key k-step of O^T += V^T.P^T for both blocks, plus both row sums (fa_agpr_asm.inc)
+template <bool kF16, int DTL>
+__device__ __forceinline__ void agpr_pv(const u32x4 *va, const u32x4 &pa, const u32x4 &pb, const u32x4 &ones) {
     if constexpr (kF16) {
-        if constexpr (DTL == 4) {
-            if constexpr (BASE == 0) fa_agpr_pv_f16_4_0(va, pf); else fa_agpr_pv_f16_4_64(va, pf);
-        } else {
-            if constexpr (BASE == 0) fa_agpr_pv_f16_2_0(va, pf); else fa_agpr_pv_f16_2_32(va, pf);
-        }
+        if constexpr (DTL == 4) fa_agpr_pv_f16_4(va, pa, pb, ones); else fa_agpr_pv_f16_2(va, pa, pb, ones);
     } else {
-        if constexpr (DTL == 4) {
-            if constexpr (BASE == 0) fa_agpr_pv_bf16_4_0(va, pf); else fa_agpr_pv_bf16_4_64(va, pf);
-        } else {
-            if constexpr (BASE == 0) fa_agpr_pv_bf16_2_0(va, pf); else fa_agpr_pv_bf16_2_32(va, pf);
-        }
+        if constexpr (DTL == 4) fa_agpr_pv_bf16_4(va, pa, pb, ones); else fa_agpr_pv_bf16_2(va, pa, pb, ones);
     }
 }
-template <int DTL, int BASE>
+template <int DTL, bool kBlockB>
 __device__ __forceinline__ void agpr_scale(const float alpha) {
     if constexpr (DTL == 4) {
-        if constexpr (BASE == 0) fa_agpr_scale_4_0(alpha); else fa_agpr_scale_4_64(alpha);
+        if constexpr (kBlockB) fa_agpr_scale_4_b(alpha); else fa_agpr_scale_4_a(alpha);
     } else {
-        if constexpr (BASE == 0) fa_agpr_scale_2_0(alpha); else fa_agpr_scale_2_32(alpha);
+        if constexpr (kBlockB) fa_agpr_scale_2_b(alpha); else fa_agpr_scale_2_a(alpha);
     }
 }
 template <int BASE>
@@ -509,11 +501,39 @@ __device__ __forceinline__ f32x16 agpr_read16() {
     else if constexpr (BASE == 64) fa_agpr_read16_64(x);
     else if constexpr (BASE == 80) fa_agpr_read16_80(x);
     else if constexpr (BASE == 96) fa_agpr_read16_96(x);
-    else fa_agpr_read16_112(x);
+    else if constexpr (BASE == 112) fa_agpr_read16_112(x);
+    else if constexpr (BASE == 128) fa_agpr_read16_128(x);
+    else fa_agpr_read16_144(x);
     f32x16 v;
 #pragma unroll
     for (int i = 0; i < 16; ++i) v[i] = x[i];
     return v;
+}
+template <int BASE>
+__device__ __forceinline__ float agpr_read1() {
+    if constexpr (BASE == 64) return fa_agpr_read1_64();
+    else if constexpr (BASE == 80) return fa_agpr_read1_80();
+    else if constexpr (BASE == 128) return fa_agpr_read1_128();
+    else return fa_agpr_read1_144();
+}
+
+// S^T += K.Q^T for both blocks, one 16-deep k-step: the K fragment pair is shared by A and B
+template <bool kF16, bool kFirst>
+__device__ __forceinline__ void mfma_s4(f32x16 &a0, f32x16 &a1, f32x16 &b0, f32x16 &b1, const u32x4 &k0,
+                                        const u32x4 &k1, const u32x4 &qa, const u32x4 &qb) {
+#define FA_S4(MF, C0, C1, C2, C3)                                                                       \
+    asm volatile(MF " %0, %4, %6, " C0 "\n\t" MF " %1, %5, %6, " C1 "\n\t" MF " %2, %4, %7, " C2 "\n\t" MF \
+                 " %3, %5, %7, " C3                                                                      \
+                 : "+v"(a0), "+v"(a1), "+v"(b0), "+v"(b1)                                                \
+                 : "v"(k0), "v"(k1), "v"(qa), "v"(qb))
+    if constexpr (kFirst) {
+        if constexpr (kF16) FA_S4("v_mfma_f32_32x32x16_f16", "0", "0", "0", "0");
+        else FA_S4("v_mfma_f32_32x32x16_bf16", "0", "0", "0", "0");
+    } else {
+        if constexpr (kF16) FA_S4("v_mfma_f32_32x32x16_f16", "%0", "%1", "%2", "%3");
+        else FA_S4("v_mfma_f32_32x32x16_bf16", "%0", "%1", "%2", "%3");
+    }
+#undef FA_S4
 }
 
 // An asm-issued MFMA's result is invisible to hipcc's hazard recognizer: before the first VALU
@@ -551,7 +571,7 @@ __device__ __forceinline__ void dma_pieces(const rsrc_t &rs, const uint32_t lds0
             "s_mov_b32 m0, %0"
             : "=&s"(keep)
             : "s"(lds0), "v"(voff[0]), "v"(voff[1]), "v"(voff[2]), "v"(voff[3]), "s"(rs)
-            : "memory");
+            : "memory", "scc");
     else
         asm volatile(
             "s_mov_b32 %0, m0\n\ts_nop 4\n\t"
@@ -560,22 +580,44 @@ __device__ __forceinline__ void dma_pieces(const rsrc_t &rs, const uint32_t lds0
             "s_mov_b32 m0, %0"
             : "=&s"(keep)
             : "s"(lds0), "v"(voff[0]), "v"(voff[1]), "s"(rs)
-            : "memory");
+            : "memory", "scc");
 }
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// =============================================================================================
+// fa_fwd_w4: one wave per SIMD, 64 query rows per wave (two 32-row blocks A and B). Per KV tile j:
+//
+//   P1(j): S_A(j), S_B(j) = K_j . Q^T   (32 MFMAs, K fragments shared)  ||  softmax part 2 of j-1
+//   P2(j): O += V_{j-1}^T . P^T(j-1)    (2*DTL+2 MFMAs per 16 keys: both blocks share the V^T
+//          fragments; the row sums of P ride on an extra MFMA with an all-ones A operand)
+//                                                                      ||  softmax part 1 of j
+//          then (rarely) rescale O and the row sums of a block whose max grew past the threshold
+//
+// MFMAs are inline asm (S into arch VGPRs, O and row sums into literal AGPRs, fa_agpr_asm.inc),
+// with slices of softmax VALU pinned between them (pin + sched_barrier). Operand fragments are
+// read from LDS one k-step ahead. S and P are double-buffered by tile parity (loop unrolled by
+// 2). K/V tiles arrive by LDS-DMA (asm buffer_load ... lds, 1 KiB per wave-instruction): K_{j+1}
+// and V_j are issued at the top of iteration j into 2-slot rings, with the XOR swizzle of the
+// LDS images applied on the per-lane SOURCE offsets; Q is DMA'd once. One barrier per tile.
+// Tiles that need masking (causal diagonal, Sk tail) run a non-pipelined body after the pipeline
+// has been drained.
+// =============================================================================================
 template <class DT, bool kCausal, int kD, bool kExactD>
-__global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const int n_qtiles) {
+__global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const int n_qtiles, const int dbg) {
     using G = Geo<kD>;
     constexpr bool F = DT::kIsF16;
     constexpr int KS = G::kKSteps;
     constexpr int DTL = G::kDTiles;
     constexpr int RB = G::kRowBytes;
-    constexpr int NP = G::kTileBytes / 4 / 1024;  // LDS-DMA pieces per wave per K or V tile (4 / 2)
+    constexpr int T = G::kTileBytes;
+    constexpr int NP = T / 4 / 1024;  // LDS-DMA pieces per wave per K or V tile (4 / 2)
     constexpr int ROWS_PER_PIECE = 1024 / RB;
-    // LDS: Q of the 4 waves (64 rows each) | K slots 0,1 | V slots 0,1,2
-    constexpr int QB = 4 * G::kTileBytes;
-    __shared__ __attribute__((aligned(1024))) char lds[QB + 5 * G::kTileBytes];
+    constexpr int LA = 32 * DTL, LB = 32 * DTL + 16;  // row-sum accumulators (AGPR bases)
+    // LDS: K slots 0,1 | V slots 0,1 | Q of the 4 waves (64 rows each). K and V sit below 64 KiB
+    // so every fragment read is a per-lane base plus a 16-bit immediate offset.
+    constexpr int KV0 = 0;
+    constexpr int QOFF = 4 * T;
+    __shared__ __attribute__((aligned(1024))) char lds[QOFF + 4 * T];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -615,18 +657,19 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         const int nb = x <= 0 ? 0 : (x + kBlockN - 1) / kBlockN;
         n_end = min(nb, n_blocks);
     }
-    // leading tiles with no masked score for any row of this wave (pipelined body)
+    // leading tiles with no masked score for any row of the WORKGROUP (pipelined; the same count
+    // for all waves keeps the LDS ring and the barriers aligned)
     int n_pipe = Sk / kBlockN;
     if (kCausal) {
-        const int x = mw + diag + 1;  // keys visible to the wave's first row
+        const int x = m0 + diag + 1;  // keys visible to the workgroup's first row
         n_pipe = min(n_pipe, x <= 0 ? 0 : x / kBlockN);
     }
     n_pipe = min(n_pipe, n_end);
+    if (dbg & 1) n_pipe = 0;  // debug: every tile through the non-pipelined body
 
     // ---- Q: this wave's 64 rows go to LDS once (LDS-DMA, K-style swizzle on the source side) --
     const int qs = (int)p.q_seqlen_stride;
-    char *const Qw = lds + wave * G::kTileBytes;
-    typedef __attribute__((address_space(3))) void lds_void;
+    char *const Qw = lds + QOFF + wave * T;
     {
         const rsrc_t qr = make_rsrc(qb + 2 * (int64_t)mw * qs, slab_bytes(min(Sq - mw, 64), qs, D));
         int qoff[4 * NP];
@@ -653,13 +696,15 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         kvo[n] = (kExactD || kch * 8 < D) ? row * ks_ * 2 + 16 * kch : 0x7ffffff0;
         vvo[n] = (kExactD || vch * 8 < D) ? row * vs_ * 2 + 16 * vch : 0x7ffffff0;
     }
-    auto stage = [&](const int j, const int kslot, const int vslot) {
+    auto stage_k = [&](const int j) {
         const int key0 = j * kBlockN;
-        const int rows = min(Sk - key0, kBlockN);
-        const rsrc_t kr = make_rsrc(kb + 2 * (int64_t)key0 * ks_, slab_bytes(rows, ks_, D));
-        const rsrc_t vr = make_rsrc(vb + 2 * (int64_t)key0 * vs_, slab_bytes(rows, vs_, D));
-        dma_pieces<NP>(kr, lds_u32(lds + QB + kslot * G::kTileBytes) + wave * NP * 1024, kvo);
-        dma_pieces<NP>(vr, lds_u32(lds + QB + (2 + vslot) * G::kTileBytes) + wave * NP * 1024, vvo);
+        const rsrc_t kr = make_rsrc(kb + 2 * (int64_t)key0 * ks_, slab_bytes(min(Sk - key0, kBlockN), ks_, D));
+        dma_pieces<NP>(kr, lds_u32(lds + KV0 + (j & 1) * T) + wave * NP * 1024, kvo);
+    };
+    auto stage_v = [&](const int j) {
+        const int key0 = j * kBlockN;
+        const rsrc_t vr = make_rsrc(vb + 2 * (int64_t)key0 * vs_, slab_bytes(min(Sk - key0, kBlockN), vs_, D));
+        dma_pieces<NP>(vr, lds_u32(lds + KV0 + (2 + (j & 1)) * T) + wave * NP * 1024, vvo);
     };
 
     // ---- per-lane LDS read addresses -----------------------------------------------------
@@ -673,50 +718,104 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     int k_addr[KS];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) k_addr[ks] = G::k_off(r, 2 * ks + h);
+    // Q fragment addresses (above 64 KiB, so absolute per k-step; block B is +32 rows)
+    int q_addr[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) q_addr[ks] = (int)lds_u32(Qw) + k_addr[ks];
+    typedef __attribute__((address_space(3))) const u32x4 lds_u32x4;
+    auto qread = [&](int ks, int boff) { return *(lds_u32x4 *)(uintptr_t)(q_addr[ks] + boff); };
+    const uint32_t one2 = DT::pack(1.f, 1.f);
+    const u32x4 ones = {one2, one2, one2, one2};
 
-    // ---- per-block state -----------------------------------------------------------------
-    // O^T of block A lives in a[0 : 16*DTL), of block B in a[16*DTL : 32*DTL) (fa_agpr_asm.inc)
-    constexpr int BASE_A = 0, BASE_B = 16 * DTL;
-    struct Blk {
-        f32x16 s0, s1;   // S^T of the current tile (keys 0-31 / 32-63)
-        u32x4 pf[4];     // P rounded to T, B operand of P.V (k-step kk = (kt, s))
-        float m, msc, l, alpha, ls;
+    // ---- state ------------------------------------------------------------------------------
+    struct Sm {   // online-softmax state of one block
+        float m, msc, alpha, part;  // running max (unscaled), m*sc, last alpha, partial max
         bool resc;
     };
-    Blk A, B;
-    if constexpr (DTL == 4) fa_agpr_zero_128(); else fa_agpr_zero_64();
-    A.m = B.m = kNeg;
-    A.msc = B.msc = 0.f;
-    A.l = B.l = 0.f;
-    A.alpha = B.alpha = 1.f;
-    A.resc = B.resc = false;
+    Sm A = {kNeg, 0.f, 1.f, 0.f, false}, B = {kNeg, 0.f, 1.f, 0.f, false};
+    f32x16 S[2][4];  // [tile parity][A keys 0-31, A 32-63, B 0-31, B 32-63]
+    u32x4 P[2][8];   // [tile parity][A k-steps 0..3, B k-steps 0..3]
+    if constexpr (DTL == 4) fa_agpr_zero_4(); else fa_agpr_zero_2();
 
-    // S^T of one block: fragment reads one k-step ahead of the MFMAs; `slice(ks)` is VALU work of
-    // the other block placed after k-step ks's MFMA pair
-    auto qk = [&](const char *K, const char *Qb, Blk &X, auto &&slice) {
-        u32x4 a0[2], a1[2], qv[2];
-        a0[0] = *(const u32x4 *)(K + k_addr[0]);
-        a1[0] = *(const u32x4 *)(K + 32 * RB + k_addr[0]);
-        qv[0] = *(const u32x4 *)(Qb + k_addr[0]);
+    // softmax part 1 of one block, slice `part` of 4: max (0, 1), decision (1), P of keys 0-31
+    // (2: keys 0-15, 3: keys 16-31) into pf[0], pf[1]
+    auto sm1 = [&](Sm &X, f32x16 &s0, f32x16 &s1, u32x4 *pf, const int part) {
+        if (part == 0) {
+            pin(X.part);
+            float m_ = fmaxf(s0[0], fmaxf(s0[1], s1[0]));
+            m_ = fmaxf(m_, fmaxf(s1[1], s0[2]));
+#pragma unroll
+            for (int i = 3; i < 8; ++i) m_ = fmaxf(m_, fmaxf(s0[i], s1[i - 1]));
+            X.part = fmaxf(m_, s1[7]);
+            pin(X.part);
+        } else if (part == 1) {
+            pin(X.part);
+            float mx = X.part;
+#pragma unroll
+            for (int i = 8; i < 16; ++i) mx = fmaxf(mx, fmaxf(s0[i], s1[i]));
+            mx = pair_max(mx);
+            X.resc = __builtin_amdgcn_ballot_w64(mx > X.m + thr_raw) != 0;
+            const float m_new = X.resc ? fmaxf(X.m, mx) : X.m;
+            // m_new * sc, or 0 while the row has seen no visible key (branch-free)
+            const float seen = m_new > 0.5f * kNeg ? 1.f : 0.f;
+            const float msc_new = X.resc ? m_new * sc * seen : X.msc;
+            X.alpha = __builtin_amdgcn_exp2f(X.msc - msc_new);
+            X.m = m_new;
+            X.msc = msc_new;
+            pin(X.msc);
+            pin(X.alpha);
+        } else {
+            const int i0 = (part - 2) * 8;
+            pin(X.msc);
+#pragma unroll
+            for (int i = i0; i < i0 + 8; ++i) s0[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s0[i], sc, -X.msc));
+            pf[part - 2] = (u32x4){DT::pack(s0[i0 + 0], s0[i0 + 1]), DT::pack(s0[i0 + 2], s0[i0 + 3]),
+                                   DT::pack(s0[i0 + 4], s0[i0 + 5]), DT::pack(s0[i0 + 6], s0[i0 + 7])};
+            pin(pf[part - 2]);
+        }
+    };
+    // softmax part 2 of one block, slice `part` of KS: P of keys 32-63 into pf[2], pf[3]
+    auto sm2 = [&](const Sm &X, f32x16 &s1, u32x4 *pf, const int part) {
+        constexpr int per = 16 / KS;  // 2 (D=128) or 4 (D=64) scores per slice
+        const int i0 = part * per;
+        float msc = X.msc;
+        pin(msc);
+#pragma unroll
+        for (int i = i0; i < i0 + per; ++i) s1[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s1[i], sc, -msc));
+        if ((i0 + per) % 8 == 0) {
+            const int q0 = i0 + per - 8;
+            pf[2 + q0 / 8] = (u32x4){DT::pack(s1[q0 + 0], s1[q0 + 1]), DT::pack(s1[q0 + 2], s1[q0 + 3]),
+                                     DT::pack(s1[q0 + 4], s1[q0 + 5]), DT::pack(s1[q0 + 6], s1[q0 + 7])};
+            pin(pf[2 + q0 / 8]);
+        }
+    };
+
+    // P1 for tile parity C: S[C] = K.Q^T for both blocks; slice(ks) after each k-step
+    auto qk = [&](const char *K, f32x16 *Sc, auto &&slice) {
+        u32x4 k0[2], k1[2], qa[2], qbv[2];
+        k0[0] = *(const u32x4 *)(K + k_addr[0]);
+        k1[0] = *(const u32x4 *)(K + 32 * RB + k_addr[0]);
+        qa[0] = qread(0, 0);
+        qbv[0] = qread(0, 32 * RB);
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             const int c = ks & 1, nx = c ^ 1;
             if (ks + 1 < KS) {
-                a0[nx] = *(const u32x4 *)(K + k_addr[ks + 1]);
-                a1[nx] = *(const u32x4 *)(K + 32 * RB + k_addr[ks + 1]);
-                qv[nx] = *(const u32x4 *)(Qb + k_addr[ks + 1]);
+                k0[nx] = *(const u32x4 *)(K + k_addr[ks + 1]);
+                k1[nx] = *(const u32x4 *)(K + 32 * RB + k_addr[ks + 1]);
+                qa[nx] = qread(ks + 1, 0);
+                qbv[nx] = qread(ks + 1, 32 * RB);
             }
             if (ks == 0)
-                mfma_s<F, true>(X.s0, X.s1, a0[c], a1[c], qv[c]);
+                mfma_s4<F, true>(Sc[0], Sc[1], Sc[2], Sc[3], k0[c], k1[c], qa[c], qbv[c]);
             else
-                mfma_s<F, false>(X.s0, X.s1, a0[c], a1[c], qv[c]);
+                mfma_s4<F, false>(Sc[0], Sc[1], Sc[2], Sc[3], k0[c], k1[c], qa[c], qbv[c]);
             slice(ks);
             FA_SCHED_FENCE();
         }
     };
-    // O^T += V^T.P^T of one block: 4 groups of DTL MFMAs, V fragments one group ahead;
-    // `slice(kk)` is VALU work of the other block placed after group kk
-    auto pv = [&](const char *V, Blk &X, auto BASE, auto &&slice) {
+    // P2: O^T += V^T.P^T for both blocks (+ row sums); slice(kk) after each 16-key k-step
+    auto pv = [&](const char *V, const u32x4 *Pp, auto &&slice) {
         u32x4 va[2][DTL];
         auto rd = [&](int kk, u32x4 *dst) {
             const int rowoff = ((kk >> 1) * 32 + (kk & 1) * 16) * RB;
@@ -731,182 +830,131 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
             if (kk + 1 < 4) rd(kk + 1, va[(kk + 1) & 1]);
-            agpr_pv<F, DTL, decltype(BASE)::value>(va[kk & 1], X.pf[kk]);
+            agpr_pv<F, DTL>(va[kk & 1], Pp[kk], Pp[4 + kk], ones);
             slice(kk);
             FA_SCHED_FENCE();
         }
     };
-
-    // softmax part 1 (4 slices): row max, deferred-rescale decision, P of keys 0-31
-    auto sm1 = [&](Blk &X, const int part) {
-        if (part == 0) {
-            s_ready(X.s0, X.s1);
-            pin(X.ls);
-            float m0_ = fmaxf(fmaxf(X.s0[0], X.s0[1]), fmaxf(X.s1[0], X.s1[1]));
-#pragma unroll
-            for (int i = 2; i < 8; i += 2) m0_ = fmaxf(m0_, fmaxf(fmaxf(X.s0[i], X.s0[i + 1]), fmaxf(X.s1[i], X.s1[i + 1])));
-            X.ls = m0_;  // partial max parked in ls
-            pin(X.ls);
-        } else if (part == 1) {
-            pin(X.ls);
-            float mx = X.ls;
-#pragma unroll
-            for (int i = 8; i < 16; i += 2) mx = fmaxf(mx, fmaxf(fmaxf(X.s0[i], X.s0[i + 1]), fmaxf(X.s1[i], X.s1[i + 1])));
-            mx = pair_max(mx);
-            X.resc = __builtin_amdgcn_ballot_w64(mx > X.m + thr_raw) != 0;
-            const float m_new = X.resc ? fmaxf(X.m, mx) : X.m;
-            const float msc_new = X.resc ? ((m_new <= kNeg) ? 0.f : m_new * sc) : X.msc;
-            X.alpha = __builtin_amdgcn_exp2f(X.msc - msc_new);
-            X.m = m_new;
-            X.msc = msc_new;
-            pin(X.msc);
-            pin(X.alpha);
-        } else {
-            const int i0 = (part - 2) * 8;  // keys i0..i0+7 of sub-tile 0 -> pf[(part-2)]
-            pin(X.msc);
-#pragma unroll
-            for (int i = i0; i < i0 + 8; ++i) X.s0[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(X.s0[i], sc, -X.msc));
-            float ls = X.s0[i0];
-#pragma unroll
-            for (int i = i0 + 1; i < i0 + 8; ++i) ls += X.s0[i];
-            X.pf[part - 2] = (u32x4){DT::pack(X.s0[i0 + 0], X.s0[i0 + 1]), DT::pack(X.s0[i0 + 2], X.s0[i0 + 3]),
-                                     DT::pack(X.s0[i0 + 4], X.s0[i0 + 5]), DT::pack(X.s0[i0 + 6], X.s0[i0 + 7])};
-            pin(X.pf[part - 2]);
-            if (part == 2) {
-                X.ls = ls;
-                pin(X.ls);
-            } else {
-                X.l = X.l * X.alpha + (X.ls + ls);
-                pin(X.l);
-            }
-        }
-    };
-    // softmax part 2 (KS slices): P of keys 32-63
-    auto sm2 = [&](Blk &X, const int part) {
-        constexpr int per = 16 / KS;  // values per slice (2 for D=128, 4 for D=64)
-        const int i0 = part * per;
-        pin(X.msc);
-#pragma unroll
-        for (int i = i0; i < i0 + per; ++i) X.s1[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(X.s1[i], sc, -X.msc));
-        float ls = X.s1[i0];
-#pragma unroll
-        for (int i = i0 + 1; i < i0 + per; ++i) ls += X.s1[i];
-        X.ls = (part == 0) ? ls : X.ls + ls;
-        pin(X.ls);
-        if ((i0 + per) % 8 == 0) {
-            const int q0 = i0 + per - 8;
-            X.pf[2 + q0 / 8] = (u32x4){DT::pack(X.s1[q0 + 0], X.s1[q0 + 1]), DT::pack(X.s1[q0 + 2], X.s1[q0 + 3]),
-                                       DT::pack(X.s1[q0 + 4], X.s1[q0 + 5]), DT::pack(X.s1[q0 + 6], X.s1[q0 + 7])};
-            pin(X.pf[2 + q0 / 8]);
-        }
-        if (part == KS - 1) {
-            X.l += X.ls;
-            pin(X.l);
-        }
-    };
-    // rare path: O *= alpha in place in the AGPRs
-    auto rescale = [&](Blk &X, auto BASE) { agpr_scale<DTL, decltype(BASE)::value>(X.alpha); };
-    auto mask = [&](Blk &X, const int key0, const int row) {
-        const int lim = kCausal ? min(Sk - 1, row + diag) : Sk - 1;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int kk = key0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-            if (kk > lim) X.s0[i] = kNeg;
-            if (kk + 32 > lim) X.s1[i] = kNeg;
-        }
+    auto rescale = [&]() {
+        if (A.resc) agpr_scale<DTL, false>(A.alpha);
+        if (B.resc) agpr_scale<DTL, true>(B.alpha);
     };
     auto none = [](int) {};
 
     // ---- prologue -------------------------------------------------------------------------
-    // B's "previous tile" in the first pipelined iteration is empty: S = kNeg gives P = 0, and its
-    // P.V reads V slot 2, zeroed here so that 0 * V stays 0.
+    // tile -1 of the pipeline is empty: its S = kNeg gives P = 0, and its P.V reads V slot 1,
+    // zeroed here so that 0 * V stays 0.
 #pragma unroll
-    for (int i = 0; i < 16; ++i) B.s1[i] = kNeg;
+    for (int i = 0; i < 16; ++i) {
+        S[1][1][i] = kNeg;
+        S[1][3][i] = kNeg;
+    }
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) B.pf[kk] = (u32x4){0, 0, 0, 0};
-    B.ls = 0.f;
+    for (int i = 0; i < 8; ++i) P[1][i] = (u32x4){0, 0, 0, 0};
     {
-        constexpr int per_thread = G::kTileBytes / 256 / 16;
+        constexpr int per_thread = T / 256 / 16;
 #pragma unroll
-        for (int i = 0; i < per_thread; ++i)
-            *(u32x4 *)(lds + QB + 4 * G::kTileBytes + (i * 256 + tid) * 16) = (u32x4){0, 0, 0, 0};
+        for (int i = 0; i < per_thread; ++i) *(u32x4 *)(lds + KV0 + 3 * T + (i * 256 + tid) * 16) = (u32x4){0, 0, 0, 0};
     }
-    if (n_end > 0) stage(0, 0, 0);
-    dma_wait();       // Q and tile 0 landed
-    __syncthreads();  // tile 0 and the zero slot visible to every wave
-    const char *const QA = Qw;
-    const char *const QBk = Qw + 32 * RB;
+    if (n_end > 0) stage_k(0);
+    dma_wait();       // Q and K_0 landed
+    __syncthreads();  // visible to every wave
 
-    // ---- pipelined tiles -----------------------------------------------------------------
-    int vprev = 2;  // V slot of tile j-1 (the zeroed slot before the first tile)
-    int j = 0;
-    for (; j < n_pipe; ++j) {
-        const int kslot = j & 1;
-        const int vcur = vprev == 2 ? 0 : vprev + 1;
-        const int vnext = vcur == 2 ? 0 : vcur + 1;
-        if (j + 1 < n_end) stage(j + 1, kslot ^ 1, vnext);
-        const char *K = lds + QB + kslot * G::kTileBytes;
-        const char *Vp = lds + QB + (2 + vprev) * G::kTileBytes;
-        const char *Vc = lds + QB + (2 + vcur) * G::kTileBytes;
-
-        qk(K, QA, A, [&](int ks) { sm2(B, ks); });           // phase 1
-        pv(Vp, B, IC<BASE_B>{}, [&](int kk) { sm1(A, kk); });   // phase 2
-        if (A.resc) rescale(A, IC<BASE_A>{});
-        qk(K, QBk, B, [&](int ks) { sm2(A, ks); });          // phase 3
-        pv(Vc, A, IC<BASE_A>{}, [&](int kk) { sm1(B, kk); });   // phase 4
-        if (B.resc) rescale(B, IC<BASE_B>{});
-
-        dma_wait();       // tile j+1 landed
+    // ---- pipelined tiles --------------------------------------------------------------------
+    auto iter = [&](const int j, auto PAR) {
+        constexpr int c = decltype(PAR)::value, pr = c ^ 1;
+        if (j + 1 < n_end) stage_k(j + 1);
+        stage_v(j);
+        const char *K = lds + KV0 + c * T;         // K_j
+        const char *Vp = lds + KV0 + (2 + pr) * T;  // V_{j-1}
+        qk(K, S[c], [&](int ks) {                   // P1
+            sm2(A, S[pr][1], P[pr], ks);
+            sm2(B, S[pr][3], P[pr] + 4, ks);
+        });
+        pv(Vp, P[pr], [&](int kk) {                 // P2
+            sm1(A, S[c][0], S[c][1], P[c], kk);
+            sm1(B, S[c][2], S[c][3], P[c] + 4, kk);
+        });
+        rescale();
+        dma_wait();  // K_{j+1}, V_j landed
         __syncthreads();
-        vprev = vcur;
+    };
+    for (int j = 0; j < n_pipe; j += 2) {
+        iter(j, IC<0>{});
+        if (j + 1 < n_pipe) iter(j + 1, IC<1>{});
     }
-    if (n_pipe > 0) {  // drain: B's softmax part 2 and P.V of the last pipelined tile
+    // drain the last pipelined tile: softmax part 2 and P.V
+    auto drain = [&](auto PAR) {
+        constexpr int c = decltype(PAR)::value;
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) sm2(B, ks);
-        pv(lds + QB + (2 + vprev) * G::kTileBytes, B, IC<BASE_B>{}, none);
+        for (int ks = 0; ks < KS; ++ks) {
+            sm2(A, S[c][1], P[c], ks);
+            sm2(B, S[c][3], P[c] + 4, ks);
+        }
+        pv(lds + KV0 + (2 + c) * T, P[c], none);
+    };
+    if (n_pipe > 0) {
+        if ((n_pipe - 1) & 1) drain(IC<1>{}); else drain(IC<0>{});
     }
 
-    // ---- remaining tiles: masked and/or partially idle, not pipelined ---------------------
-    for (; j < n_end; ++j) {
-        const int kslot = j & 1;
-        const int vcur = vprev == 2 ? 0 : vprev + 1;
-        const int vnext = vcur == 2 ? 0 : vcur + 1;
-        if (j + 1 < n_end) stage(j + 1, kslot ^ 1, vnext);
-        const char *K = lds + QB + kslot * G::kTileBytes;
-        const char *Vc = lds + QB + (2 + vcur) * G::kTileBytes;
-        const int key0 = j * kBlockN;
-        auto full = [&](Blk &X, const char *Qx, const int row, auto BASE) {
-            qk(K, Qx, X, none);
-            s_ready(X.s0, X.s1);
-            mask(X, key0, row);
-#pragma unroll
-            for (int part = 0; part < 4; ++part) sm1(X, part);
-            if (X.resc) rescale(X, BASE);
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) sm2(X, ks);
-            pv(Vc, X, BASE, none);
-        };
-        if (!kCausal || key0 <= mw + 31 + diag) full(A, QA, mw + r, IC<BASE_A>{});
-        if (!kCausal || key0 <= mw + 63 + diag) full(B, QBk, mw + 32 + r, IC<BASE_B>{});
+    // ---- remaining tiles: masked, not pipelined --------------------------------------------
+    if (n_pipe < n_end) {
+        stage_v(n_pipe);  // the pipeline fetched V one tile late; catch up before the first one
         dma_wait();
         __syncthreads();
-        vprev = vcur;
+    }
+    for (int j = n_pipe; j < n_end; ++j) {
+        if (j + 1 < n_end) {
+            stage_k(j + 1);
+            stage_v(j + 1);
+        }
+        const char *K = lds + KV0 + (j & 1) * T;
+        const char *V = lds + KV0 + (2 + (j & 1)) * T;
+        const int key0 = j * kBlockN;
+        qk(K, S[0], none);
+        s_ready(S[0][0], S[0][1]);
+        s_ready(S[0][2], S[0][3]);
+        auto mask = [&](f32x16 &s0, f32x16 &s1, const int row) {
+            const int lim = kCausal ? min(Sk - 1, row + diag) : Sk - 1;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int kk = key0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                if (kk > lim) s0[i] = kNeg;
+                if (kk + 32 > lim) s1[i] = kNeg;
+            }
+        };
+        mask(S[0][0], S[0][1], mw + r);
+        mask(S[0][2], S[0][3], mw + 32 + r);
+#pragma unroll
+        for (int part = 0; part < 4; ++part) {
+            sm1(A, S[0][0], S[0][1], P[0], part);
+            sm1(B, S[0][2], S[0][3], P[0] + 4, part);
+        }
+        rescale();
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            sm2(A, S[0][1], P[0], ks);
+            sm2(B, S[0][3], P[0] + 4, ks);
+        }
+        pv(V, P[0], none);
+        dma_wait();
+        __syncthreads();
     }
 
     // ---- epilogue ---------------------------------------------------------------------------
     mfma_drain();  // last asm MFMA -> AGPR reads
     const int os_ = (int)p.o_seqlen_stride;
     const rsrc_t orr = make_rsrc(ob + 2 * (int64_t)mw * os_, slab_bytes(min(Sq - mw, 64), os_, D));
-    auto store_block = [&](const Blk &X, const int row, auto BASE) {
-        constexpr int base = decltype(BASE)::value;
+    auto store_block = [&](const int row, auto OBASE, auto LBASE) {
+        constexpr int ob0 = decltype(OBASE)::value;
         f32x16 o[DTL];
-        o[0] = agpr_read16<base>();
-        o[1] = agpr_read16<base + 16>();
+        o[0] = agpr_read16<ob0>();
+        o[1] = agpr_read16<ob0 + 16>();
         if constexpr (DTL == 4) {
-            o[2] = agpr_read16<base + 32>();
-            o[3] = agpr_read16<base + 48>();
+            o[2] = agpr_read16<ob0 + 32>();
+            o[3] = agpr_read16<ob0 + 48>();
         }
-        const float l_tot = pair_sum(X.l);
+        const float l_tot = agpr_read1<decltype(LBASE)::value>();
         const float inv = (l_tot == 0.f) ? 1.f : 1.f / l_tot;
         const int orow = row * os_ * 2;
 #pragma unroll
@@ -926,8 +974,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             }
         }
     };
-    store_block(A, r, IC<BASE_A>{});
-    store_block(B, r + 32, IC<BASE_B>{});
+    store_block(r, IC<0>{}, IC<LA>{});
+    store_block(r + 32, IC<16 * DTL>{}, IC<LB>{});
 }
 
 }  // namespace fa
@@ -992,19 +1040,22 @@ int check_params(const fa_fwd_params *p, int dtype, int causal) {
 // 8-wave register-staged kernel (kept for A/B measurements and as a cross-check in the tests).
 int variant_from_env() {
     const char *v = getenv("FA_GFX950_VARIANT");
-    return (v && strcmp(v, "w8") == 0) ? 1 : 0;
+    if (v && strcmp(v, "w8") == 0) return 1;
+    if (v && strcmp(v, "w4slow") == 0) return 2;  // debug: w4 without the pipelined body
+    return 0;
 }
 
 template <class DT, bool C, int kD, bool kExact>
 int launch_one(const fa_fwd_params &p, hipStream_t stream) {
     const int64_t n_qtiles = (p.seqlen_q + fa::kBlockM - 1) / fa::kBlockM;
     const int64_t nwg = n_qtiles * p.num_heads_q * p.batch_size;
-    if (variant_from_env() == 1)
+    const int variant = variant_from_env();
+    if (variant == 1)
         hipLaunchKernelGGL((fa::fa_fwd_w8<DT, C, kD, kExact>), dim3((uint32_t)nwg), dim3(fa::kThreads), 0, stream, p,
                            (int)n_qtiles);
     else
         hipLaunchKernelGGL((fa::fa_fwd_w4<DT, C, kD, kExact>), dim3((uint32_t)nwg), dim3(256), 0, stream, p,
-                           (int)n_qtiles);
+                           (int)n_qtiles, variant == 2 ? 1 : 0);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "HIP launch failed: %s", hipGetErrorString(e));
     return FA_OK;

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Dump the main-loop instruction mix of one kernel instantiation (host-side, no GPU).
 # usage: scripts/asm_loop.sh [mangled-kernel-regex] [source]
-K=${1:-_ZN2fa13fa_fwd_kernelINS_3F16ELb0ELi128ELb1EEEv13fa_fwd_paramsi}
+K=${1:-_ZN2fa9fa_fwd_w4INS_3F16ELb0ELi128ELb1EEEv13fa_fwd_paramsii}
 SRC=${2:-/root/repo/flash_attention_cute_amd/csrc/fa_fwd_gfx950.hip}
 D=/root/repo/build/asm; mkdir -p $D; cd $D
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -include stdarg.h -I/root/repo/include \

@@ -7,7 +7,7 @@ import sys
 agg = collections.defaultdict(list)
 for f in glob.glob(f"{sys.argv[1]}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "fa_fwd_kernel" in r["Kernel_Name"]:
+        if "fa::fa_fwd" in r["Kernel_Name"]:
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k in sorted(agg):
     v = agg[k]
