@@ -64,6 +64,14 @@ template <int N>
 struct IC {
     static constexpr int value = N;
 };
+// compile-time loop: f(IC<I>{}) for I = 0 .. N-1 (every index a constant expression)
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(F &&f) {
+    if constexpr (I < N) {
+        f(IC<I>{});
+        static_for<N, I + 1>(f);
+    }
+}
 
 struct F16 {
     static constexpr bool kIsF16 = true;
@@ -452,36 +460,18 @@ __global__ __launch_bounds__(kThreads) void fa_fwd_w8(const fa_fwd_params p, con
 // non-pipelined body after the pipeline has been drained.
 // =============================================================================================
 
-// S += A.B for the two 32-key sub-tiles (same Q fragment); kFirst: C = 0.
-template <bool kF16, bool kFirst>
-__device__ __forceinline__ void mfma_s(f32x16 &s0, f32x16 &s1, const u32x4 &a0, const u32x4 &a1, const u32x4 &q) {
-    if constexpr (kFirst) {
-        if constexpr (kF16)
-            asm volatile("v_mfma_f32_32x32x16_f16 %0, %2, %4, 0\n\tv_mfma_f32_32x32x16_f16 %1, %3, %4, 0"
-                         : "=&v"(s0), "=&v"(s1) : "v"(a0), "v"(a1), "v"(q));
-        else
-            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %2, %4, 0\n\tv_mfma_f32_32x32x16_bf16 %1, %3, %4, 0"
-                         : "=&v"(s0), "=&v"(s1) : "v"(a0), "v"(a1), "v"(q));
-    } else {
-        if constexpr (kF16)
-            asm volatile("v_mfma_f32_32x32x16_f16 %0, %2, %4, %0\n\tv_mfma_f32_32x32x16_f16 %1, %3, %4, %1"
-                         : "+v"(s0), "+v"(s1) : "v"(a0), "v"(a1), "v"(q));
-        else
-            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %2, %4, %0\n\tv_mfma_f32_32x32x16_bf16 %1, %3, %4, %1"
-                         : "+v"(s0), "+v"(s1) : "v"(a0), "v"(a1), "v"(q));
-    }
-}
-
 #include "fa_agpr_asm.inc"
 
-// one 16-key k-step of O^T += V^T.P^T for both blocks, plus both row sums (fa_agpr_asm.inc)
-template <bool kF16, int DTL>
-__device__ __forceinline__ void agpr_pv(const u32x4 *va, const u32x4 &pa, const u32x4 &pb, const u32x4 &ones) {
-    if constexpr (kF16) {
-        if constexpr (DTL == 4) fa_agpr_pv_f16_4(va, pa, pb, ones); else fa_agpr_pv_f16_2(va, pa, pb, ones);
-    } else {
-        if constexpr (DTL == 4) fa_agpr_pv_bf16_4(va, pa, pb, ones); else fa_agpr_pv_bf16_2(va, pa, pb, ones);
+// one MFMA a[BASE..BASE+15] += A.B into literal AGPRs (fa_agpr_asm.inc)
+template <bool kF16, int BASE>
+__device__ __forceinline__ void agpr_mfma(const u32x4 &a, const u32x4 &b) {
+#define FA_CASE(N)                                                    \
+    if constexpr (BASE == N) {                                        \
+        if constexpr (kF16) fa_agpr_mfma_f16_##N(a, b);               \
+        else fa_agpr_mfma_bf16_##N(a, b);                             \
     }
+    FA_CASE(0) FA_CASE(16) FA_CASE(32) FA_CASE(48) FA_CASE(64) FA_CASE(80) FA_CASE(96) FA_CASE(112)
+#undef FA_CASE
 }
 template <int DTL, bool kBlockB>
 __device__ __forceinline__ void agpr_scale(const float alpha) {
@@ -517,23 +507,17 @@ __device__ __forceinline__ float agpr_read1() {
     else return fa_agpr_read1_144();
 }
 
-// S^T += K.Q^T for both blocks, one 16-deep k-step: the K fragment pair is shared by A and B
-template <bool kF16, bool kFirst>
-__device__ __forceinline__ void mfma_s4(f32x16 &a0, f32x16 &a1, f32x16 &b0, f32x16 &b1, const u32x4 &k0,
-                                        const u32x4 &k1, const u32x4 &qa, const u32x4 &qb) {
-#define FA_S4(MF, C0, C1, C2, C3)                                                                       \
-    asm volatile(MF " %0, %4, %6, " C0 "\n\t" MF " %1, %5, %6, " C1 "\n\t" MF " %2, %4, %7, " C2 "\n\t" MF \
-                 " %3, %5, %7, " C3                                                                      \
-                 : "+v"(a0), "+v"(a1), "+v"(b0), "+v"(b1)                                                \
-                 : "v"(k0), "v"(k1), "v"(qa), "v"(qb))
-    if constexpr (kFirst) {
-        if constexpr (kF16) FA_S4("v_mfma_f32_32x32x16_f16", "0", "0", "0", "0");
-        else FA_S4("v_mfma_f32_32x32x16_bf16", "0", "0", "0", "0");
+// one MFMA of S^T = K.Q^T into arch VGPRs (inline asm, so hipcc keeps it in program order among
+// the softmax slices); first: C = 0
+template <bool kF16>
+__device__ __forceinline__ void mfma_sv(const bool first, f32x16 &acc, const u32x4 &a, const u32x4 &b) {
+    if (first) {
+        if constexpr (kF16) asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "v"(b));
+        else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "v"(b));
     } else {
-        if constexpr (kF16) FA_S4("v_mfma_f32_32x32x16_f16", "%0", "%1", "%2", "%3");
-        else FA_S4("v_mfma_f32_32x32x16_bf16", "%0", "%1", "%2", "%3");
+        if constexpr (kF16) asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+        else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
     }
-#undef FA_S4
 }
 
 // An asm-issued MFMA's result is invisible to hipcc's hazard recognizer: before the first VALU
@@ -549,6 +533,7 @@ __device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 7\n\ts_nop 7\
 // so IR-level sinking / hoisting cannot move the VALU slices out of their MFMA gap.
 __device__ __forceinline__ void pin(float &x) { asm volatile("" : "+v"(x)); }
 __device__ __forceinline__ void pin(u32x4 &x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(uint32_t &x) { asm volatile("" : "+v"(x)); }
 
 __device__ __forceinline__ uint32_t lds_u32(const void *ptr) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)ptr;
@@ -581,6 +566,19 @@ __device__ __forceinline__ void dma_pieces(const rsrc_t &rs, const uint32_t lds0
             : "=&s"(keep)
             : "s"(lds0), "v"(voff[0]), "v"(voff[1]), "s"(rs)
             : "memory", "scc");
+}
+// one LDS-DMA piece (1 KiB per wave-instruction) from rs + voff to LDS lds; nop: 5 wait states
+// ahead of the descriptor read (a VALU write of those SGPRs is invisible to the hazard recognizer)
+__device__ __forceinline__ void dma_one(const rsrc_t &rs, const uint32_t lds, const int voff, const bool nop) {
+    uint32_t keep;
+    if (nop)
+        asm volatile("s_mov_b32 %0, m0\n\ts_nop 4\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                     "buffer_load_dwordx4 %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "s"(lds), "v"(voff), "s"(rs) : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                     "buffer_load_dwordx4 %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "s"(lds), "v"(voff), "s"(rs) : "memory");
 }
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
@@ -724,122 +722,221 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     for (int ks = 0; ks < KS; ++ks) q_addr[ks] = (int)lds_u32(Qw) + k_addr[ks];
     typedef __attribute__((address_space(3))) const u32x4 lds_u32x4;
     auto qread = [&](int ks, int boff) { return *(lds_u32x4 *)(uintptr_t)(q_addr[ks] + boff); };
-    const uint32_t one2 = DT::pack(1.f, 1.f);
-    const u32x4 ones = {one2, one2, one2, one2};
-
     // ---- state ------------------------------------------------------------------------------
-    struct Sm {   // online-softmax state of one block
-        float m, msc, alpha, part;  // running max (unscaled), m*sc, last alpha, partial max
+    struct Sm {               // online-softmax state of one block (per lane: one query row)
+        float m, msc, alpha;  // running max (unscaled), m*sc, alpha of the last decision
+        float mE, mO;         // two max chains over the tile being reduced (mE then holds m_new)
+        float l, t;           // this lane's half of the row sum over finished tiles; s0 sum of the
+                              // tile being reduced (new scale, folded into l at the rescale)
         bool resc;
     };
-    Sm A = {kNeg, 0.f, 1.f, 0.f, false}, B = {kNeg, 0.f, 1.f, 0.f, false};
-    f32x16 S[2][4];  // [tile parity][A keys 0-31, A 32-63, B 0-31, B 32-63]
-    u32x4 P[2][8];   // [tile parity][A k-steps 0..3, B k-steps 0..3]
+    Sm st[2];
+#pragma unroll
+    for (int X = 0; X < 2; ++X) st[X] = {kNeg, 0.f, 1.f, kNeg, kNeg, 0.f, 0.f, false};
+    f32x16 S[2][4];  // [tile parity][2 * block + half]: half 0 = keys 0-31, 1 = keys 32-63
+    u32x4 P[2][8];   // [tile parity][4 * block + k-step]
     if constexpr (DTL == 4) fa_agpr_zero_4(); else fa_agpr_zero_2();
 
-    // softmax part 1 of one block, slice `part` of 4: max (0, 1), decision (1), P of keys 0-31
-    // (2: keys 0-15, 3: keys 16-31) into pf[0], pf[1]
-    auto sm1 = [&](Sm &X, f32x16 &s0, f32x16 &s1, u32x4 *pf, const int part) {
-        if (part == 0) {
-            pin(X.part);
-            float m_ = fmaxf(s0[0], fmaxf(s0[1], s1[0]));
-            m_ = fmaxf(m_, fmaxf(s1[1], s0[2]));
-#pragma unroll
-            for (int i = 3; i < 8; ++i) m_ = fmaxf(m_, fmaxf(s0[i], s1[i - 1]));
-            X.part = fmaxf(m_, s1[7]);
-            pin(X.part);
-        } else if (part == 1) {
-            pin(X.part);
-            float mx = X.part;
-#pragma unroll
-            for (int i = 8; i < 16; ++i) mx = fmaxf(mx, fmaxf(s0[i], s1[i]));
-            mx = pair_max(mx);
-            X.resc = __builtin_amdgcn_ballot_w64(mx > X.m + thr_raw) != 0;
-            const float m_new = X.resc ? fmaxf(X.m, mx) : X.m;
-            // m_new * sc, or 0 while the row has seen no visible key (branch-free)
-            const float seen = m_new > 0.5f * kNeg ? 1.f : 0.f;
-            const float msc_new = X.resc ? m_new * sc * seen : X.msc;
-            X.alpha = __builtin_amdgcn_exp2f(X.msc - msc_new);
-            X.m = m_new;
-            X.msc = msc_new;
-            pin(X.msc);
-            pin(X.alpha);
+    // ---- softmax units (each a few VALU instructions, placed between single MFMAs) ----------
+    // max chain unit i (0..15) of block X: scores i of both halves
+    auto u_max = [&](const int c, const int X, const int i) {
+        const f32x16 &s0 = S[c][2 * X], &s1 = S[c][2 * X + 1];
+        float &mm = (i & 1) ? st[X].mO : st[X].mE;
+        mm = (i < 2) ? fmaxf(s0[i], s1[i]) : fmaxf(mm, fmaxf(s0[i], s1[i]));
+        pin(mm);
+    };
+    // the rescale decision of block X in two units: the row max and m_new; then m*sc and alpha
+    auto u_dec = [&](const int X, const int k) {
+        Sm &Z = st[X];
+        if (k == 0) {
+            const float mx = pair_max(fmaxf(Z.mE, Z.mO));
+            Z.resc = __builtin_amdgcn_ballot_w64(mx > Z.m + thr_raw) != 0;
+            Z.mE = Z.resc ? fmaxf(Z.m, mx) : Z.m;
+            pin(Z.mE);
         } else {
-            const int i0 = (part - 2) * 8;
-            pin(X.msc);
-#pragma unroll
-            for (int i = i0; i < i0 + 8; ++i) s0[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s0[i], sc, -X.msc));
-            pf[part - 2] = (u32x4){DT::pack(s0[i0 + 0], s0[i0 + 1]), DT::pack(s0[i0 + 2], s0[i0 + 3]),
-                                   DT::pack(s0[i0 + 4], s0[i0 + 5]), DT::pack(s0[i0 + 6], s0[i0 + 7])};
-            pin(pf[part - 2]);
+            const float m_new = Z.mE;
+            const float seen = m_new > 0.5f * kNeg ? 1.f : 0.f;  // m_new * sc, or 0 before any visible key
+            const float msc_new = Z.resc ? m_new * sc * seen : Z.msc;
+            Z.alpha = __builtin_amdgcn_exp2f(Z.msc - msc_new);
+            Z.m = m_new;
+            Z.msc = msc_new;
+            pin(Z.msc);
+            pin(Z.alpha);
         }
     };
-    // softmax part 2 of one block, slice `part` of KS: P of keys 32-63 into pf[2], pf[3]
-    auto sm2 = [&](const Sm &X, f32x16 &s1, u32x4 *pf, const int part) {
-        constexpr int per = 16 / KS;  // 2 (D=128) or 4 (D=64) scores per slice
-        const int i0 = part * per;
-        float msc = X.msc;
-        pin(msc);
-#pragma unroll
-        for (int i = i0; i < i0 + per; ++i) s1[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s1[i], sc, -msc));
-        if ((i0 + per) % 8 == 0) {
-            const int q0 = i0 + per - 8;
-            pf[2 + q0 / 8] = (u32x4){DT::pack(s1[q0 + 0], s1[q0 + 1]), DT::pack(s1[q0 + 2], s1[q0 + 3]),
-                                     DT::pack(s1[q0 + 4], s1[q0 + 5]), DT::pack(s1[q0 + 6], s1[q0 + 7])};
-            pin(pf[2 + q0 / 8]);
-        }
+    // P = exp2(s * sc - m * sc) of score v of half hf of block X, in place
+    auto u_exp = [&](const int c, const int X, const int hf, const int v) {
+        f32x16 &s = S[c][2 * X + hf];
+        float x = __builtin_amdgcn_exp2f(__builtin_fmaf(s[v], sc, -st[X].msc));
+        pin(x);
+        s[v] = x;
     };
-
-    // P1 for tile parity C: S[C] = K.Q^T for both blocks; slice(ks) after each k-step
-    auto qk = [&](const char *K, f32x16 *Sc, auto &&slice) {
-        u32x4 k0[2], k1[2], qa[2], qbv[2];
-        k0[0] = *(const u32x4 *)(K + k_addr[0]);
-        k1[0] = *(const u32x4 *)(K + 32 * RB + k_addr[0]);
-        qa[0] = qread(0, 0);
-        qbv[0] = qread(0, 32 * RB);
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            const int c = ks & 1, nx = c ^ 1;
-            if (ks + 1 < KS) {
-                k0[nx] = *(const u32x4 *)(K + k_addr[ks + 1]);
-                k1[nx] = *(const u32x4 *)(K + 32 * RB + k_addr[ks + 1]);
-                qa[nx] = qread(ks + 1, 0);
-                qbv[nx] = qread(ks + 1, 32 * RB);
-            }
-            if (ks == 0)
-                mfma_s4<F, true>(Sc[0], Sc[1], Sc[2], Sc[3], k0[c], k1[c], qa[c], qbv[c]);
-            else
-                mfma_s4<F, false>(Sc[0], Sc[1], Sc[2], Sc[3], k0[c], k1[c], qa[c], qbv[c]);
-            slice(ks);
-            FA_SCHED_FENCE();
-        }
-    };
-    // P2: O^T += V^T.P^T for both blocks (+ row sums); slice(kk) after each 16-key k-step
-    auto pv = [&](const char *V, const u32x4 *Pp, auto &&slice) {
-        u32x4 va[2][DTL];
-        auto rd = [&](int kk, u32x4 *dst) {
-            const int rowoff = ((kk >> 1) * 32 + (kk & 1) * 16) * RB;
-#pragma unroll
-            for (int dt = 0; dt < DTL; ++dt) {
-                const u32x2 lo = tr_read(V + rowoff + v_addr[dt]);
-                const u32x2 hi = tr_read(V + rowoff + 8 * RB + v_addr[dt]);
-                dst[dt] = (u32x4){lo[0], lo[1], hi[0], hi[1]};
-            }
-        };
-        rd(0, va[0]);
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-            if (kk + 1 < 4) rd(kk + 1, va[(kk + 1) & 1]);
-            agpr_pv<F, DTL>(va[kk & 1], Pp[kk], Pp[4 + kk], ones);
-            slice(kk);
-            FA_SCHED_FENCE();
+    // row sum of P (half 0 -> t, half 1 -> l) and, for odd v, the rounded pair (v-1, v) into the
+    // P.V operand of its 16-key k-step
+    auto u_fin = [&](const int c, const int X, const int hf, const int v) {
+        const f32x16 &s = S[c][2 * X + hf];
+        float &acc = hf ? st[X].l : st[X].t;
+        acc = (hf == 0 && v == 0) ? s[0] : acc + s[v];
+        pin(acc);
+        if (v & 1) {
+            uint32_t w = DT::pack(s[v - 1], s[v]);
+            pin(w);
+            P[c][4 * X + 2 * hf + (v >> 3)][(v & 7) >> 1] = w;
         }
     };
     auto rescale = [&]() {
-        if (A.resc) agpr_scale<DTL, false>(A.alpha);
-        if (B.resc) agpr_scale<DTL, true>(B.alpha);
+        if (st[0].resc) agpr_scale<DTL, false>(st[0].alpha);
+        if (st[1].resc) agpr_scale<DTL, true>(st[1].alpha);
+#pragma unroll
+        for (int X = 0; X < 2; ++X) st[X].l = __builtin_fmaf(st[X].l, st[X].alpha, st[X].t);
     };
-    auto none = [](int) {};
+
+    // ---- phase 1: S[c] = K.Q^T for both blocks (4*KS single MFMAs) ----------------------------
+    // gap g (after MFMA g): next k-step's K / Q fragments (gaps 4ks, 4ks+1), one LDS-DMA piece
+    // (gap 4ks+2: K_{j+1} pieces, then V_j pieces), and with SM2 the second softmax half of the
+    // tile of parity pr (32 units: block u&1, score u>>1 of half 1).
+    constexpr int G1 = 4 * KS;
+    auto phase1 = [&](const char *K, auto PAR, auto SM2, auto DMA, const rsrc_t &kr, const rsrc_t &vr,
+                      const uint32_t k_lds, const uint32_t v_lds) {
+        constexpr int c = decltype(PAR)::value, pr = c ^ 1;
+        constexpr bool do_sm = decltype(SM2)::value, do_dma = decltype(DMA)::value;
+        u32x4 kf[2][2], qf[2][2];  // [buffer][key half | block]
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+            kf[0][x] = *(const u32x4 *)(K + x * 32 * RB + k_addr[0]);
+            qf[0][x] = qread(0, x * 32 * RB);
+        }
+        static_for<G1>([&](auto G) {
+            constexpr int g = decltype(G)::value;
+            constexpr int ks = g >> 2, i = g & 3, cb = ks & 1;
+            mfma_sv<F>(ks == 0, S[c][i], kf[cb][i & 1], qf[cb][i >> 1]);
+            if constexpr (ks + 1 < KS && i < 2) {
+                kf[cb ^ 1][i] = *(const u32x4 *)(K + i * 32 * RB + k_addr[ks + 1]);
+                qf[cb ^ 1][i] = qread(ks + 1, i * 32 * RB);
+            }
+            if constexpr (do_dma && i == 2) {
+                if constexpr (ks < NP) dma_one(kr, k_lds + ks * 1024, kvo[ks], ks == 0);
+                else dma_one(vr, v_lds + (ks - NP) * 1024, vvo[ks - NP], ks == NP);
+            }
+            if constexpr (do_sm) {
+                static_for<32>([&](auto U) {
+                    constexpr int u = decltype(U)::value;
+                    if constexpr ((u * G1) / 32 == g) {
+                        u_exp(pr, u & 1, 1, u >> 1);
+                        if constexpr (u >= 2) u_fin(pr, u & 1, 1, (u >> 1) - 1);
+                    }
+                });
+            }
+            FA_SCHED_FENCE();
+        });
+        if constexpr (do_sm) {
+            u_fin(pr, 0, 1, 15);
+            u_fin(pr, 1, 1, 15);
+        }
+    };
+    // the same second softmax half without MFMAs (drain and masked tiles)
+    auto sm2_all = [&](auto PAR) {
+        constexpr int c = decltype(PAR)::value;
+        static_for<16>([&](auto VV) {
+            constexpr int v = decltype(VV)::value;
+            static_for<2>([&](auto XX) {
+                u_exp(c, decltype(XX)::value, 1, v);
+                u_fin(c, decltype(XX)::value, 1, v);
+            });
+        });
+    };
+
+    // ---- phase 2: O^T += V^T.P^T for both blocks (8*DTL single MFMAs into the AGPRs) ----------
+    // gap g (kk = g / 2DTL, i = g % 2DTL; MFMA: block i / DTL, d-tile i % DTL): V^T read i of
+    // k-step kk+1, and with SM1 the first softmax half of the tile of parity cs (schedule below).
+    constexpr int G2 = 8 * DTL;
+    constexpr int GQ = G2 / 8;  // 4 (D=128) / 2 (D=64)
+    // exp unit e (0..31) -> block / score: A0..A4, then B and A alternating, then B11..B15
+    struct Ex {  // exp unit e (0..31) -> block / score: A0..A4, then B and A alternating, then B11..B15
+        static constexpr int blk(int e) { return e < 5 ? 0 : (e < 27 ? (((e - 5) & 1) ? 0 : 1) : 1); }
+        static constexpr int v(int e) {
+            return e < 5 ? e : (e < 27 ? (((e - 5) & 1) ? 5 + ((e - 5) >> 1) : (e - 5) >> 1) : 11 + (e - 27));
+        }
+        static constexpr int gap(int e) { return GQ + 2 + (e * (G2 - GQ - 2)) / 32; }
+        static constexpr int max_gap(int X, int m) { return X * GQ + (m * GQ) / 16; }
+        static constexpr int dec_gap(int X, int k) { return (X + 1) * GQ + (GQ == 2 ? 0 : k); }
+    };
+    static_assert([] {  // the schedule respects max -> decision -> exp of each block, and fits
+        for (int X = 0; X < 2; ++X) {
+            if (Ex::dec_gap(X, 0) < Ex::max_gap(X, 15) || Ex::dec_gap(X, 1) < Ex::dec_gap(X, 0)) return false;
+            if (Ex::max_gap(X, 15) >= G2) return false;
+        }
+        for (int e = 0; e < 32; ++e) {
+            if (Ex::gap(e) < Ex::dec_gap(Ex::blk(e), 1) || Ex::gap(e) >= G2) return false;
+            if (e > 0 && Ex::gap(e) < Ex::gap(e - 1)) return false;
+        }
+        return true;
+    }(), "phase-2 softmax schedule");
+    auto phase2 = [&](const char *V, auto PPV, auto PSM, auto SM1) {
+        constexpr int cp = decltype(PPV)::value, cs = decltype(PSM)::value;
+        constexpr bool do_sm = decltype(SM1)::value;
+        u32x4 va[2][DTL];
+        auto rd = [&](const int kk, const int n, u32x4 *dst) {
+            const int rowoff = ((kk >> 1) * 32 + (kk & 1) * 16) * RB + (n & 1) * 8 * RB;
+            const u32x2 x = tr_read(V + rowoff + v_addr[n >> 1]);
+            dst[n >> 1][2 * (n & 1)] = x[0];
+            dst[n >> 1][2 * (n & 1) + 1] = x[1];
+        };
+#pragma unroll
+        for (int n = 0; n < 2 * DTL; ++n) rd(0, n, va[0]);
+        static_for<G2>([&](auto G) {
+            constexpr int g = decltype(G)::value;
+            constexpr int kk = g / (2 * DTL), i = g % (2 * DTL), X = i / DTL, dt = i % DTL;
+            agpr_mfma<F, X * 16 * DTL + 16 * dt>(va[kk & 1][dt], P[cp][4 * X + kk]);
+            if constexpr (kk + 1 < 4) rd(kk + 1, i, va[(kk + 1) & 1]);
+            if constexpr (do_sm) {
+                static_for<32>([&](auto M) {
+                    constexpr int X2 = decltype(M)::value >> 4, m = decltype(M)::value & 15;
+                    if constexpr (Ex::max_gap(X2, m) == g) u_max(cs, X2, m);
+                });
+                static_for<4>([&](auto K2) {
+                    constexpr int X2 = decltype(K2)::value >> 1, k = decltype(K2)::value & 1;
+                    if constexpr (Ex::dec_gap(X2, k) == g) u_dec(X2, k);
+                });
+                static_for<32>([&](auto E) {
+                    constexpr int e = decltype(E)::value;
+                    if constexpr (Ex::gap(e) + 1 == g) u_fin(cs, Ex::blk(e), 0, Ex::v(e));
+                    if constexpr (Ex::gap(e) == g) u_exp(cs, Ex::blk(e), 0, Ex::v(e));
+                });
+            }
+            FA_SCHED_FENCE();
+        });
+        if constexpr (do_sm) {
+            static_for<32>([&](auto E) {
+                constexpr int e = decltype(E)::value;
+                if constexpr (Ex::gap(e) == G2 - 1) u_fin(cs, Ex::blk(e), 0, Ex::v(e));
+            });
+        }
+    };
+    // the same first softmax half without MFMAs (masked tiles)
+    auto sm1_all = [&](auto PAR) {
+        constexpr int c = decltype(PAR)::value;
+        static_for<2>([&](auto XX) {
+            constexpr int X = decltype(XX)::value;
+            static_for<16>([&](auto M) { u_max(c, X, decltype(M)::value); });
+            u_dec(X, 0);
+            u_dec(X, 1);
+            static_for<16>([&](auto VV) {
+                u_exp(c, X, 0, decltype(VV)::value);
+                u_fin(c, X, 0, decltype(VV)::value);
+            });
+        });
+    };
+
+    auto k_rsrc = [&](const int j) {
+        const int key0 = j * kBlockN;
+        return make_rsrc(kb + 2 * (int64_t)key0 * ks_, slab_bytes(min(Sk - key0, kBlockN), ks_, D));
+    };
+    auto v_rsrc = [&](const int j) {
+        const int key0 = j * kBlockN;
+        return make_rsrc(vb + 2 * (int64_t)key0 * vs_, slab_bytes(min(Sk - key0, kBlockN), vs_, D));
+    };
+    const uint32_t lds_base = lds_u32(lds) + wave * NP * 1024;  // this wave's pieces of slot 0
 
     // ---- prologue -------------------------------------------------------------------------
     // tile -1 of the pipeline is empty: its S = kNeg gives P = 0, and its P.V reads V slot 1,
@@ -860,21 +957,13 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     dma_wait();       // Q and K_0 landed
     __syncthreads();  // visible to every wave
 
-    // ---- pipelined tiles --------------------------------------------------------------------
+    // ---- pipelined tiles: iteration j = P1(S_j || softmax half 2 of j-1, DMA K_{j+1}, V_j),
+    //      P2(O += P_{j-1} V_{j-1} || softmax half 1 of j), rescale, barrier -------------------
     auto iter = [&](const int j, auto PAR) {
         constexpr int c = decltype(PAR)::value, pr = c ^ 1;
-        if (j + 1 < n_end) stage_k(j + 1);
-        stage_v(j);
-        const char *K = lds + KV0 + c * T;         // K_j
-        const char *Vp = lds + KV0 + (2 + pr) * T;  // V_{j-1}
-        qk(K, S[c], [&](int ks) {                   // P1
-            sm2(A, S[pr][1], P[pr], ks);
-            sm2(B, S[pr][3], P[pr] + 4, ks);
-        });
-        pv(Vp, P[pr], [&](int kk) {                 // P2
-            sm1(A, S[c][0], S[c][1], P[c], kk);
-            sm1(B, S[c][2], S[c][3], P[c] + 4, kk);
-        });
+        const rsrc_t kr = k_rsrc(j + 1), vr = v_rsrc(j);
+        phase1(lds + KV0 + c * T, PAR, IC<1>{}, IC<1>{}, kr, vr, lds_base + pr * T, lds_base + (2 + c) * T);
+        phase2(lds + KV0 + (2 + pr) * T, IC<pr>{}, PAR, IC<1>{});
         rescale();
         dma_wait();  // K_{j+1}, V_j landed
         __syncthreads();
@@ -883,15 +972,11 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         iter(j, IC<0>{});
         if (j + 1 < n_pipe) iter(j + 1, IC<1>{});
     }
-    // drain the last pipelined tile: softmax part 2 and P.V
+    // drain the last pipelined tile: softmax half 2 and P.V
     auto drain = [&](auto PAR) {
         constexpr int c = decltype(PAR)::value;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            sm2(A, S[c][1], P[c], ks);
-            sm2(B, S[c][3], P[c] + 4, ks);
-        }
-        pv(lds + KV0 + (2 + c) * T, P[c], none);
+        sm2_all(PAR);
+        phase2(lds + KV0 + (2 + c) * T, PAR, PAR, IC<0>{});
     };
     if (n_pipe > 0) {
         if ((n_pipe - 1) & 1) drain(IC<1>{}); else drain(IC<0>{});
@@ -911,7 +996,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         const char *K = lds + KV0 + (j & 1) * T;
         const char *V = lds + KV0 + (2 + (j & 1)) * T;
         const int key0 = j * kBlockN;
-        qk(K, S[0], none);
+        phase1(K, IC<0>{}, IC<0>{}, IC<0>{}, k_rsrc(j), k_rsrc(j), 0u, 0u);
         s_ready(S[0][0], S[0][1]);
         s_ready(S[0][2], S[0][3]);
         auto mask = [&](f32x16 &s0, f32x16 &s1, const int row) {
@@ -925,18 +1010,10 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         };
         mask(S[0][0], S[0][1], mw + r);
         mask(S[0][2], S[0][3], mw + 32 + r);
-#pragma unroll
-        for (int part = 0; part < 4; ++part) {
-            sm1(A, S[0][0], S[0][1], P[0], part);
-            sm1(B, S[0][2], S[0][3], P[0] + 4, part);
-        }
+        sm1_all(IC<0>{});
         rescale();
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            sm2(A, S[0][1], P[0], ks);
-            sm2(B, S[0][3], P[0] + 4, ks);
-        }
-        pv(V, P[0], none);
+        sm2_all(IC<0>{});
+        phase2(V, IC<0>{}, IC<0>{}, IC<0>{});
         dma_wait();
         __syncthreads();
     }
@@ -945,7 +1022,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     mfma_drain();  // last asm MFMA -> AGPR reads
     const int os_ = (int)p.o_seqlen_stride;
     const rsrc_t orr = make_rsrc(ob + 2 * (int64_t)mw * os_, slab_bytes(min(Sq - mw, 64), os_, D));
-    auto store_block = [&](const int row, auto OBASE, auto LBASE) {
+    auto store_block = [&](const int row, auto OBASE, const float l_lane) {
         constexpr int ob0 = decltype(OBASE)::value;
         f32x16 o[DTL];
         o[0] = agpr_read16<ob0>();
@@ -954,7 +1031,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             o[2] = agpr_read16<ob0 + 32>();
             o[3] = agpr_read16<ob0 + 48>();
         }
-        const float l_tot = agpr_read1<decltype(LBASE)::value>();
+        const float l_tot = pair_sum(l_lane);
         const float inv = (l_tot == 0.f) ? 1.f : 1.f / l_tot;
         const int orow = row * os_ * 2;
 #pragma unroll
@@ -974,8 +1051,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             }
         }
     };
-    store_block(r, IC<0>{}, IC<LA>{});
-    store_block(r + 32, IC<16 * DTL>{}, IC<LB>{});
+    store_block(r, IC<0>{}, st[0].l);
+    store_block(r + 32, IC<16 * DTL>{}, st[1].l);
 }
 
 }  // namespace fa
