@@ -5,8 +5,10 @@ drives nvcc through ``torch.utils.cpp_extension.load`` and, under ROCm torch, hi
 files into the source tree. Here nothing is hipified: two explicit compiler invocations write
 into the package directory so the artefacts travel with the repository snapshot.
 
-  1. ``hipcc --offload-arch=gfx950``  csrc/fa_fwd_gfx950.hip  ->  lib/libfa_gfx950.so
-     (the C-ABI library of include/fa_gfx950.h; no torch symbols)
+  1. ``hipcc --offload-arch=gfx950``  csrc/fa_inst.hip x 16 (one object per dtype x causal x
+     head-dim tile x exact-D instantiation, compiled in parallel) + csrc/fa_fwd_gfx950.hip (C-ABI
+     dispatcher)  ->  lib/libfa_gfx950.so (the C-ABI library of include/fa_gfx950.h; no torch
+     symbols)
   2. ``g++``  csrc/flash_attention_api.cpp  ->  _C<ext>.so  (pybind11 torch binding, linked
      against lib/libfa_gfx950.so with an $ORIGIN rpath)
 
@@ -55,22 +57,52 @@ def _run(cmd: list[str], verbose: bool) -> None:
 
 
 def abi_sources() -> list[Path]:
-    return [CSRC / "fa_fwd_gfx950.hip", INCLUDE / "fa_gfx950.h", Path(__file__).resolve()]
+    return [CSRC / "fa_fwd_gfx950.hip", CSRC / "fa_fwd_kernels.hpp", CSRC / "fa_launch.h", CSRC / "fa_inst.hip",
+            CSRC / "fa_agpr_asm.inc", INCLUDE / "fa_gfx950.h", Path(__file__).resolve()]
+
+
+# (dtype, causal, head-dim tile, exact head dim): must match FA_FOR_EACH_INSTANCE in csrc/fa_launch.h
+INSTANCES = [(dt, c, d, e) for dt in ("F16", "BF16") for c in (0, 1) for d in (64, 128) for e in (0, 1)]
+
+HIP_FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-mcode-object-version=5",
+             "-ffinite-math-only", "-fno-signed-zeros"]
+
+
+def _jobs() -> int:
+    n = os.environ.get("MAX_JOBS") or os.cpu_count() or 4
+    return max(1, min(int(n), 16))
 
 
 def build_abi(force: bool = False, verbose: bool = False) -> Path:
-    """Compile the HIP kernels + C-ABI into lib/libfa_gfx950.so (gfx950 code object)."""
+    """Compile the HIP kernels + C-ABI into lib/libfa_gfx950.so (gfx950 code objects).
+
+    Each kernel instantiation is its own translation unit (csrc/fa_inst.hip with -D selectors), so
+    the 16 device compiles run in parallel; objects go to build/ and are linked by hipcc.
+    """
+    from concurrent.futures import ThreadPoolExecutor
+
     LIBDIR.mkdir(exist_ok=True)
     if not force and not _stale(ABI_LIB, abi_sources()):
         return ABI_LIB
     if not HIPCC.exists():
         raise RuntimeError(f"hipcc not found at {HIPCC}")
+    objdir = ROOT / "build" / "obj"
+    objdir.mkdir(parents=True, exist_ok=True)
+    cmds = []
+    objs = []
+    for dt, c, d, e in INSTANCES:
+        obj = objdir / f"fa_inst_{dt.lower()}_c{c}_d{d}_x{e}.o"
+        objs.append(obj)
+        cmds.append([HIPCC, *HIP_FLAGS, f"-I{INCLUDE}", f"-I{CSRC}", f"-DFA_INST_DT={dt}", f"-DFA_INST_CAUSAL={c}",
+                     f"-DFA_INST_D={d}", f"-DFA_INST_EXACT={e}", "-c", CSRC / "fa_inst.hip", "-o", obj])
+    disp = objdir / "fa_fwd_gfx950.o"
+    objs.append(disp)
+    cmds.append([HIPCC, *HIP_FLAGS, f"-I{INCLUDE}", f"-I{CSRC}", "-c", CSRC / "fa_fwd_gfx950.hip", "-o", disp])
+    with ThreadPoolExecutor(max_workers=_jobs()) as ex:
+        for f in [ex.submit(_run, cmd, verbose) for cmd in cmds]:
+            f.result()
     tmp = ABI_LIB.with_suffix(".so.tmp")
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-mcode-object-version=5", "-ffinite-math-only", "-fno-signed-zeros",
-           "-include", "stdarg.h", f"-I{INCLUDE}",
-           CSRC / "fa_fwd_gfx950.hip", "-o", tmp]
-    _run(cmd, verbose)
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp], verbose)
     os.replace(tmp, ABI_LIB)
     return ABI_LIB
 

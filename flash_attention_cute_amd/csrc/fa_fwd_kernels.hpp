@@ -1,0 +1,1077 @@
+#pragma once
+// fa_fwd_kernels.hpp -- FlashAttention-2 forward kernels for MI355X (gfx950 / CDNA4).
+//
+// Device code only. Each (dtype, causal, head-dim tile, exact-D) combination is instantiated in
+// its own translation unit (fa_inst.hip, compiled once per combination by _build.py, in
+// parallel); fa_fwd_gfx950.hip holds the C-ABI and the runtime dispatch.
+//
+// Replaces, MI355X-first (not a translation):
+//   reference csrc/flash_attention_template.cuh:138-564  flash_attention_v2 (CuTe, mma.sync, 4 warps)
+//   reference csrc/mask.cuh:30-88                        Mask (OOB + bottom-right causal)
+//   reference csrc/flash_attention_impl.cu:7-49          tile choice + 4 specialisations
+//   reference csrc/kernel_dispatcher.h:20-52             dtype / headdim / causal dispatch
+//
+// Design (DESIGN.md section 3 has the numbers):
+//   * one workgroup = 8 wave64s = 256 query rows of one (batch, q-head); each wave owns 32 rows;
+//   * KV tiles of 64 keys are register-staged (global_load_dwordx4 issued one tile ahead)
+//     into a double-buffered LDS ring (K and V, 16 KiB each per buffer, 64 KiB total);
+//   * S^T = K . Q^T with v_mfma_f32_32x32x16_{f16,bf16}: A = K rows from LDS (ds_read_b128,
+//     XOR-swizzled), B = Q^T held in VGPRs for the whole KV loop. Each lane then owns ONE query
+//     and 32 of the tile's 64 keys, so the row max / row sum are in-lane plus a single
+//     v_permlane32_swap (the reference needs a 4-lane shuffle butterfly, template.cuh:72-88);
+//   * O^T += V^T . P^T with the same MFMA: the S^T accumulator, rounded to T, is directly the
+//     B operand (no LDS round trip, no lane movement); V^T comes from ds_read_b64_tr_b16
+//     transposed LDS reads of a row-major, XOR-swizzled V tile;
+//   * O^T keeps the query on the lane, so the online-softmax rescale is a per-lane scalar;
+//   * masking only on KV tiles that cross the causal diagonal or the Sk tail, and a wave skips
+//     KV tiles that are fully masked for its 32 rows;
+//   * workgroup ids are remapped so that the q-tiles of one kv-head group run on one XCD
+//     (blocks b and b+8 share an XCD), keeping the K/V stream in that XCD's 4 MiB L2.
+//
+// Numerics follow the reference (Appendix A of SURVEY.md): S accumulated in fp32, max taken on
+// unscaled S, P = exp2(S*s' - m*s') with s' = scale*log2(e) precomputed by the host, P rounded
+// (RNE) to T before P.V, row sums of the fp32 P, O / l with l == 0 -> 1. Fully masked rows
+// (causal with Sq > Sk) are defined as 0 (DESIGN.md "quirks").
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "fa_gfx950.h"
+#include "fa_launch.h"
+
+namespace fa {
+
+// Masked / not-yet-seen scores use a large finite sentinel instead of -inf so that the kernel can
+// be compiled without IEEE inf/NaN semantics (no canonicalising v_max before fmaxf, v_max3).
+constexpr float kNeg = -1.0e30f;
+// Deferred rescale (guide T13): the running max used for exp2 is only raised when a row's max grows
+// by more than kRescaleThr (log2 units, i.e. a factor 2^8) -- P then stays <= 256, exact in fp16 /
+// bf16 relative precision, and the O / l rescale pass is skipped on almost every tile.
+constexpr float kRescaleThr = 8.0f;
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+template <int N>
+struct IC {
+    static constexpr int value = N;
+};
+// compile-time loop: f(IC<I>{}) for I = 0 .. N-1 (every index a constant expression)
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(F &&f) {
+    if constexpr (I < N) {
+        f(IC<I>{});
+        static_for<N, I + 1>(f);
+    }
+}
+
+struct F16 {
+    static constexpr bool kIsF16 = true;
+    static __device__ __forceinline__ f32x16 mfma(u32x4 a, u32x4 b, f32x16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a),
+                                                      __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+    }
+    // round-to-nearest-even pack of two fp32 into two fp16 (low element first): v_cvt_pk_f16_f32
+    static __device__ __forceinline__ uint32_t pack(float lo, float hi) {
+        f16x2 v = __builtin_convertvector((f32x2){lo, hi}, f16x2);
+        return __builtin_bit_cast(uint32_t, v);
+    }
+};
+
+struct BF16 {
+    static constexpr bool kIsF16 = false;
+    static __device__ __forceinline__ f32x16 mfma(u32x4 a, u32x4 b, f32x16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                       __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+    }
+    // v_cvt_pk_bf16_f32 (RNE)
+    static __device__ __forceinline__ uint32_t pack(float lo, float hi) {
+        bf16x2 v = __builtin_convertvector((f32x2){lo, hi}, bf16x2);
+        return __builtin_bit_cast(uint32_t, v);
+    }
+};
+
+// Per head-dim geometry. kD is the padded head dim of the LDS image and of the MFMA k-steps.
+template <int kD>
+struct Geo {
+    static constexpr int kRowBytes = kD * 2;            // 256 / 128
+    static constexpr int kChunks = kD / 8;              // 16-B chunks per row
+    static constexpr int kTileBytes = kBlockN * kRowBytes;
+    // LDS ring: 2 K slots + 3 V slots. V needs a third slot because waves 4-7 run their P.V of
+    // tile j after the barrier that publishes tile j+1 (see "stagger" in the kernel).
+    static constexpr int kLdsBytes = 5 * kTileBytes;
+    static constexpr int kKSteps = kD / 16;             // k-steps of S^T = K.Q^T
+    static constexpr int kDTiles = kD / 32;             // 32-row d tiles of O^T
+    static constexpr int kStage = kBlockN * kChunks / kThreads;  // chunks per thread per tile (2 / 1)
+
+    // K image: the A-operand read has lane r on row r (one 16-B chunk each). For 256-B rows the
+    // chunk slot is c ^ (r & 15); for 128-B rows (two rows per 256-B bank row) c ^ ((r >> 1) & 7).
+    // Both put the 16 lanes of every ds_read_b128 lane group on 16 distinct 16-B bank slots.
+    static __device__ __forceinline__ int k_off(int row, int ch) {
+        return kD == 128 ? row * 256 + 16 * (ch ^ (row & 15)) : row * 128 + 16 * (ch ^ ((row >> 1) & 7));
+    }
+    // V image, read transposed by ds_read_b64_tr_b16: a half-wave reads 4 rows R..R+3 (R % 4 == 0)
+    // x 64 B; the XOR puts the four 64-B pieces into the four quarters of the 256-B bank row.
+    static __device__ __forceinline__ int v_off(int row, int ch) {
+        return kD == 128 ? row * 256 + 16 * (ch ^ ((row & 3) << 2))
+                         : row * 128 + 16 * (ch ^ (((row >> 1) & 1) << 2));
+    }
+};
+
+// v_permlane32_swap(vdst=x, src=x): the lower half-wave receives the upper half's x in the src
+// result and keeps its own in vdst; the upper half the other way round. Combining both results
+// therefore gives the (l, l^32) pair reduction with the same value in both lanes.
+__device__ __forceinline__ float pair_max(float x) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float pair_sum(float x) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+__device__ __forceinline__ u32x2 tr_read(const char *lds_ptr) {
+    typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+    i16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4 *)(lds_ptr));
+    return __builtin_bit_cast(u32x2, v);
+}
+
+// Buffer descriptor over [base, base + nbytes): loads past the end return 0 and stores past the
+// end are dropped by the hardware range check, so ragged tails need no per-lane predicates.
+__device__ __forceinline__ rsrc_t make_rsrc(const char *base, uint32_t nbytes) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)nbytes, 0x00020000);
+}
+
+// bytes of the first `rows` (<= 64) rows of a [rows, D] slab with row stride `stride` elements;
+// 0 if rows <= 0. The host guarantees 64 * stride * 2 + 256 < 2^31.
+__device__ __forceinline__ uint32_t slab_bytes(int rows, int stride, int D) {
+    return rows <= 0 ? 0u : (uint32_t)(((rows - 1) * stride + D) * 2);
+}
+
+template <class DT, bool kCausal, int kD, bool kExactD>
+__global__ __launch_bounds__(kThreads) void fa_fwd_w8(const fa_fwd_params p, const int n_qtiles) {
+    using G = Geo<kD>;
+    __shared__ __attribute__((aligned(16))) char lds[G::kLdsBytes];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31;
+    const int h = lane >> 5;
+
+    // ---- XCD-aware work decode ----------------------------------------------------------
+    // Blocks are dealt round-robin over the 8 XCDs (b and b+8 share one). Remap so that each
+    // XCD walks a contiguous range of the logical order (bijective for any grid size).
+    const uint32_t nwg = gridDim.x;
+    const uint32_t bid = blockIdx.x;
+    const uint32_t xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const uint32_t w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    // logical order: batch, q-head (members of one kv group adjacent), q-tile
+    const uint32_t t = w % (uint32_t)n_qtiles;
+    const uint32_t bh = w / (uint32_t)n_qtiles;
+    const int hq = (int)(bh % (uint32_t)p.num_heads_q);
+    const int b = (int)(bh / (uint32_t)p.num_heads_q);
+    const int qtile = kCausal ? (n_qtiles - 1 - (int)t) : (int)t;  // heavy tiles first
+    const int hkv = hq / (int)p.head_q_per_group;
+
+    const int Sq = (int)p.seqlen_q, Sk = (int)p.seqlen_kv, D = (int)p.headdim;
+    const float sc = p.softmax_scale;
+    const float thr_raw = kRescaleThr / sc;  // rescale threshold in unscaled score units
+
+    const char *qb = (const char *)p.q_ptr + 2 * ((int64_t)b * p.q_batch_stride + (int64_t)hq * p.q_head_stride);
+    const char *kb = (const char *)p.k_ptr + 2 * ((int64_t)b * p.k_batch_stride + (int64_t)hkv * p.k_head_stride);
+    const char *vb = (const char *)p.v_ptr + 2 * ((int64_t)b * p.v_batch_stride + (int64_t)hkv * p.v_head_stride);
+    char *ob = (char *)p.o_ptr + 2 * ((int64_t)b * p.o_batch_stride + (int64_t)hq * p.o_head_stride);
+
+    const int m0 = qtile * kBlockM;   // first query row of the workgroup
+    const int mw = m0 + wave * 32;    // first query row of this wave
+    const int my_q = mw + r;          // this lane's query row
+    const int diag = Sk - Sq;         // bottom-right causal offset: key n visible iff n <= m + diag
+
+    // ---- KV tile range ----------------------------------------------------------------
+    const int n_blocks = (Sk + kBlockN - 1) / kBlockN;
+    int n_end = n_blocks;
+    if (kCausal) {
+        // the workgroup's last valid query sees keys up to min(m0+BM, Sq) - 1 + diag
+        const int x = diag + min(m0 + kBlockM, Sq);
+        const int nb = x <= 0 ? 0 : (x + kBlockN - 1) / kBlockN;
+        n_end = min(nb, n_blocks);
+    }
+
+    // ---- Q fragments (B operand of S^T = K.Q^T), resident for the whole loop ----------
+    // lane (h, r) holds Q[my_q][16*ks + 8*h + 0..7] for k-step ks; rows >= Sq read as 0
+    u32x4 qf[G::kKSteps];
+    {
+        const int qs = (int)p.q_seqlen_stride;
+        const rsrc_t qr = make_rsrc(qb + 2 * (int64_t)mw * qs, slab_bytes(min(Sq - mw, 32), qs, D));
+        const int off = r * qs * 2 + 16 * h;
+#pragma unroll
+        for (int ks = 0; ks < G::kKSteps; ++ks) {
+            qf[ks] = __builtin_amdgcn_raw_buffer_load_b128(qr, off + 32 * ks, 0, 0);
+            if (!kExactD && 16 * ks + 8 * h >= D) qf[ks] = (u32x4){0, 0, 0, 0};
+        }
+    }
+
+    // ---- register staging of K/V tiles ------------------------------------------------
+    // thread t moves 16-B chunk (t % kChunks) of rows t / kChunks (+ 32 for D = 128) of K and V
+    const int srow = tid / G::kChunks;
+    const int sch = tid % G::kChunks;
+    const int ks_ = (int)p.k_seqlen_stride, vs_ = (int)p.v_seqlen_stride;
+    const int koff0 = srow * ks_ * 2 + 16 * sch;
+    const int voff0 = srow * vs_ * 2 + 16 * sch;
+    const int koff1 = koff0 + 32 * ks_ * 2;
+    const int voff1 = voff0 + 32 * vs_ * 2;
+    const bool sch_ok = kExactD || sch * 8 < D;
+    u32x4 kst0, kst1, vst0, vst1;
+
+    auto stage_load = [&](int j) {
+        // descriptors rebased per tile: 32-bit lane offsets stay tile-invariant; rows >= Sk read 0
+        const int key0 = j * kBlockN;
+        const rsrc_t kr = make_rsrc(kb + 2 * (int64_t)key0 * ks_, slab_bytes(min(Sk - key0, kBlockN), ks_, D));
+        const rsrc_t vr = make_rsrc(vb + 2 * (int64_t)key0 * vs_, slab_bytes(min(Sk - key0, kBlockN), vs_, D));
+        kst0 = __builtin_amdgcn_raw_buffer_load_b128(kr, koff0, 0, 0);
+        vst0 = __builtin_amdgcn_raw_buffer_load_b128(vr, voff0, 0, 0);
+        if (G::kStage == 2) {
+            kst1 = __builtin_amdgcn_raw_buffer_load_b128(kr, koff1, 0, 0);
+            vst1 = __builtin_amdgcn_raw_buffer_load_b128(vr, voff1, 0, 0);
+        }
+    };
+    auto stage_write = [&](int kslot, int vslot) {
+        char *K = lds + kslot * G::kTileBytes;
+        char *V = lds + (2 + vslot) * G::kTileBytes;
+        // D < kD: K columns past D must be 0 (they meet Q's zero columns, garbage could be NaN)
+        const u32x4 z = {0, 0, 0, 0};
+        *(u32x4 *)(K + G::k_off(srow, sch)) = sch_ok ? kst0 : z;
+        *(u32x4 *)(V + G::v_off(srow, sch)) = vst0;
+        if (G::kStage == 2) {
+            *(u32x4 *)(K + G::k_off(srow + 32, sch)) = sch_ok ? kst1 : z;
+            *(u32x4 *)(V + G::v_off(srow + 32, sch)) = vst1;
+        }
+    };
+
+    // ---- per-lane constant LDS addresses ----------------------------------------------
+    // V^T A-operand via ds_read_b64_tr_b16: lane = 16*g + 4*qq + pp supplies row (R + qq),
+    // columns dt*32 + 16*(g&1) + 4*pp .. +3 where R = kt*32 + 16*s + 4*(g>>1) (+8 for the
+    // second half of the fragment); it receives column dt*32 + (lane & 31) of rows R..R+3.
+    const int g = lane >> 4;
+    const int qq = (lane >> 2) & 3;
+    const int pp = lane & 3;
+    int v_addr[G::kDTiles];
+#pragma unroll
+    for (int dt = 0; dt < G::kDTiles; ++dt)
+        v_addr[dt] = G::v_off(4 * (g >> 1) + qq, dt * 4 + 2 * (g & 1) + (pp >> 1)) + 8 * (pp & 1);
+    int k_addr[G::kKSteps];
+#pragma unroll
+    for (int ks = 0; ks < G::kKSteps; ++ks) k_addr[ks] = G::k_off(r, 2 * ks + h);
+
+    f32x16 o[G::kDTiles];
+#pragma unroll
+    for (int dt = 0; dt < G::kDTiles; ++dt) o[dt] = (f32x16){};
+    float m_use = kNeg;  // running max used by exp2 (unscaled score units), lags by < kRescaleThr
+    float msc = 0.f;     // m_use * sc, or 0 while the row has seen no visible key
+    float l_run = 0.f;   // lane-partial row sum of P (32 of the 64 keys of each tile)
+
+    // Stagger (MI355X_MICROARCH "Two waves per SIMD"): waves w and w+4 share a SIMD. Waves 4-7
+    // ("lag") run each tile's P.V after the tile's barrier, i.e. half a tile behind waves 0-3, so
+    // one wave's softmax (VALU) overlaps its partner's MFMAs instead of both waves alternating
+    // between all-MFMA and all-VALU phases in lockstep.
+    const bool lag = wave >= 4;
+    u32x4 pf[4];               // P of the last softmax (B operand of P.V), k-step kk = (kt, s)
+    bool pv_pending = false;   // lag waves: P.V of the previous tile still to do
+    const char *pv_v = lds;    // ... and the V slot it reads
+
+    // S^T = K.Q^T, mask, online softmax; leaves P (rounded to T) in pf
+    auto qk_softmax = [&](const char *K, const int key0, const bool need_mask) {
+        f32x16 s0 = {}, s1 = {};
+#pragma unroll
+        for (int ks = 0; ks < G::kKSteps; ++ks) {
+            const u32x4 a0 = *(const u32x4 *)(K + k_addr[ks]);
+            const u32x4 a1 = *(const u32x4 *)(K + 32 * G::kRowBytes + k_addr[ks]);
+            s0 = DT::mfma(a0, qf[ks], s0);
+            s1 = DT::mfma(a1, qf[ks], s1);
+        }
+        // mask (only tiles crossing the diagonal or the Sk tail)
+        if (need_mask) {
+            const int lim = kCausal ? min(Sk - 1, my_q + diag) : Sk - 1;  // last visible key
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int kk = key0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                if (kk > lim) s0[i] = kNeg;
+                if (kk + 32 > lim) s1[i] = kNeg;
+            }
+        }
+        // online softmax (per lane = per query row)
+        float mx = fmaxf(fmaxf(s0[0], s0[1]), fmaxf(s1[0], s1[1]));
+#pragma unroll
+        for (int i = 2; i < 16; i += 2) mx = fmaxf(mx, fmaxf(fmaxf(s0[i], s0[i + 1]), fmaxf(s1[i], s1[i + 1])));
+        mx = pair_max(mx);
+        // deferred rescale: taken by the whole wave when any row's max outgrows m_use; every
+        // earlier P.V is already in O at this point (lag waves ran theirs first)
+        float alpha = 1.f;
+        const bool grow = mx > m_use + thr_raw;
+        if (__builtin_amdgcn_ballot_w64(grow)) {
+            const float m_new = fmaxf(m_use, mx);
+            const float msc_new = (m_new <= kNeg) ? 0.f : m_new * sc;
+            alpha = __builtin_amdgcn_exp2f(msc - msc_new);  // msc == 0 && m_use == kNeg: l, O are 0
+            m_use = m_new;
+            msc = msc_new;
+#pragma unroll
+            for (int dt = 0; dt < G::kDTiles; ++dt) o[dt] *= alpha;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            s0[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s0[i], sc, -msc));
+            s1[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s1[i], sc, -msc));
+        }
+        float ls0 = s0[0], ls1 = s1[0];
+#pragma unroll
+        for (int i = 1; i < 16; ++i) {
+            ls0 += s0[i];
+            ls1 += s1[i];
+        }
+        l_run = l_run * alpha + (ls0 + ls1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            pf[s] = (u32x4){DT::pack(s0[8 * s + 0], s0[8 * s + 1]), DT::pack(s0[8 * s + 2], s0[8 * s + 3]),
+                            DT::pack(s0[8 * s + 4], s0[8 * s + 5]), DT::pack(s0[8 * s + 6], s0[8 * s + 7])};
+            pf[2 + s] = (u32x4){DT::pack(s1[8 * s + 0], s1[8 * s + 1]), DT::pack(s1[8 * s + 2], s1[8 * s + 3]),
+                                DT::pack(s1[8 * s + 4], s1[8 * s + 5]), DT::pack(s1[8 * s + 6], s1[8 * s + 7])};
+        }
+    };
+
+    // O^T += V^T . P^T
+    auto pv = [&](const char *V) {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const int rowoff = ((kk >> 1) * 32 + (kk & 1) * 16) * G::kRowBytes;  // kt*32 + 16*s
+#pragma unroll
+            for (int dt = 0; dt < G::kDTiles; ++dt) {
+                const u32x2 lo = tr_read(V + rowoff + v_addr[dt]);
+                const u32x2 hi = tr_read(V + rowoff + 8 * G::kRowBytes + v_addr[dt]);
+                o[dt] = DT::mfma((u32x4){lo[0], lo[1], hi[0], hi[1]}, pf[kk], o[dt]);
+            }
+        }
+    };
+
+    if (n_end > 0) stage_load(0);
+    // retire Q and tile 0 here; the asm barrier re-defines qf so the loop's wait analysis does not
+    // see the Q loads as pending (it would otherwise wait vmcnt(0) at the top of every iteration)
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+#pragma unroll
+    for (int ks = 0; ks < G::kKSteps; ++ks) asm volatile("" : "+v"(qf[ks]));
+    if (n_end > 0) {
+        stage_write(0, 0);
+        if (n_end > 1) stage_load(1);
+    }
+    __syncthreads();
+
+    // one KV tile; the K slot KB is a compile-time constant (loop unrolled by 2) so K addresses
+    // are a per-lane base plus an immediate offset; the V slot cycles through 3
+    int vslot = 0;
+    auto tile = [&](const int j, auto KB) {
+        constexpr int kslot = decltype(KB)::value;
+        const char *K = lds + kslot * G::kTileBytes;
+        const char *V = lds + (2 + vslot) * G::kTileBytes;
+        const int key0 = j * kBlockN;
+
+        bool wave_active = true;
+        bool need_mask = key0 + kBlockN > Sk;
+        if (kCausal) {
+            wave_active = key0 <= mw + 31 + diag;                      // a key visible to the last row
+            need_mask = need_mask || (key0 + kBlockN - 1 > mw + diag);  // a key hidden from the first row
+        }
+        if (pv_pending) {  // lag waves: previous tile's P.V (its V slot is not overwritten until j+2)
+            pv(pv_v);
+            pv_pending = false;
+        }
+        if (wave_active) {
+            qk_softmax(K, key0, need_mask);
+            if (lag) {
+                pv_pending = true;
+                pv_v = V;
+            } else {
+                pv(V);
+            }
+        }
+        vslot = vslot == 2 ? 0 : vslot + 1;
+        if (j + 1 < n_end) stage_write(kslot ^ 1, vslot);
+        __syncthreads();
+        if (j + 2 < n_end) stage_load(j + 2);
+    };
+    for (int j = 0; j < n_end; j += 2) {
+        tile(j, IC<0>{});
+        if (j + 1 < n_end) tile(j + 1, IC<1>{});
+    }
+    if (pv_pending) pv(pv_v);
+
+    // ---- epilogue: O = O^T / l, row per lane, 16-B stores after a half-wave swap ----------
+    const float l_tot = pair_sum(l_run);
+    const float inv = (l_tot == 0.f) ? 1.f : 1.f / l_tot;
+    const int os_ = (int)p.o_seqlen_stride;
+    const rsrc_t orr = make_rsrc(ob + 2 * (int64_t)mw * os_, slab_bytes(min(Sq - mw, 32), os_, D));
+    const int orow = r * os_ * 2;
+#pragma unroll
+    for (int dt = 0; dt < G::kDTiles; ++dt) {
+#pragma unroll
+        for (int gp = 0; gp < 4; gp += 2) {
+            // this lane holds d = dt*32 + 8*grp + 4*h + 0..3 in o[dt][4*grp .. 4*grp+3]
+            const uint32_t a0 = DT::pack(o[dt][4 * gp + 0] * inv, o[dt][4 * gp + 1] * inv);
+            const uint32_t a1 = DT::pack(o[dt][4 * gp + 2] * inv, o[dt][4 * gp + 3] * inv);
+            const uint32_t b0 = DT::pack(o[dt][4 * gp + 4] * inv, o[dt][4 * gp + 5] * inv);
+            const uint32_t b1 = DT::pack(o[dt][4 * gp + 6] * inv, o[dt][4 * gp + 7] * inv);
+            const auto x0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+            const auto x1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+            // lower half: d = dt*32 + 8*gp + 0..7 ; upper half: d = dt*32 + 8*(gp+1) + 0..7
+            const int d0 = dt * 32 + 8 * (gp + h);
+            if (kExactD || d0 < D)
+                __builtin_amdgcn_raw_buffer_store_b128((u32x4){x0[0], x1[0], x0[1], x1[1]}, orr, orow + 2 * d0, 0,
+                                                       0);
+        }
+    }
+}
+
+
+// =============================================================================================
+// fa_fwd_w4: one wave per SIMD, 64 query rows per wave (two 32-row blocks A and B), software
+// pipelined so that every MFMA stretch of one block runs beside the softmax VALU of the other:
+//
+//   phase 1: S_A(j)  = K_j . Q_A^T        ||  softmax part 2 of B (tile j-1)
+//   phase 2: O_B    += V_{j-1}^T . P_B^T  ||  softmax part 1 of A (tile j)   -> rescale O_A
+//   phase 3: S_B(j)  = K_j . Q_B^T        ||  softmax part 2 of A (tile j)
+//   phase 4: O_A    += V_j^T . P_A^T      ||  softmax part 1 of B (tile j)   -> rescale O_B
+//
+// Within a phase the MFMAs (inline asm, 2 or 4 per group) and slices of the other block's softmax
+// alternate in program order, pinned by sched_barrier; operand fragments are read from LDS one
+// group ahead. The O accumulators of both blocks live in AGPRs for the whole kernel (asm "+a"
+// operands); S, P, Q/K/V fragments and the softmax state stay in the 256 arch VGPRs.
+// K/V tiles arrive by LDS-DMA (buffer_load ... lds, 1 KiB per wave-instruction) issued one tile
+// ahead into a 2-slot K / 3-slot V ring; the XOR swizzle of the LDS images is applied on the
+// per-lane SOURCE offsets (the DMA destination is lane-linear). Q is DMA'd to LDS once and its
+// fragments are re-read per tile. One barrier per tile.
+// Tiles that need masking (causal diagonal, Sk tail) or where a block is idle run a plain,
+// non-pipelined body after the pipeline has been drained.
+// =============================================================================================
+
+#include "fa_agpr_asm.inc"
+
+// one MFMA a[BASE..BASE+15] += A.B into literal AGPRs (fa_agpr_asm.inc)
+template <bool kF16, int BASE>
+__device__ __forceinline__ void agpr_mfma(const u32x4 &a, const u32x4 &b) {
+#define FA_CASE(N)                                                    \
+    if constexpr (BASE == N) {                                        \
+        if constexpr (kF16) fa_agpr_mfma_f16_##N(a, b);               \
+        else fa_agpr_mfma_bf16_##N(a, b);                             \
+    }
+    FA_CASE(0) FA_CASE(16) FA_CASE(32) FA_CASE(48) FA_CASE(64) FA_CASE(80) FA_CASE(96) FA_CASE(112)
+#undef FA_CASE
+}
+template <int DTL, bool kBlockB>
+__device__ __forceinline__ void agpr_scale(const float alpha) {
+    if constexpr (DTL == 4) {
+        if constexpr (kBlockB) fa_agpr_scale_4_b(alpha); else fa_agpr_scale_4_a(alpha);
+    } else {
+        if constexpr (kBlockB) fa_agpr_scale_2_b(alpha); else fa_agpr_scale_2_a(alpha);
+    }
+}
+template <int BASE>
+__device__ __forceinline__ f32x16 agpr_read16() {
+    float x[16];
+    if constexpr (BASE == 0) fa_agpr_read16_0(x);
+    else if constexpr (BASE == 16) fa_agpr_read16_16(x);
+    else if constexpr (BASE == 32) fa_agpr_read16_32(x);
+    else if constexpr (BASE == 48) fa_agpr_read16_48(x);
+    else if constexpr (BASE == 64) fa_agpr_read16_64(x);
+    else if constexpr (BASE == 80) fa_agpr_read16_80(x);
+    else if constexpr (BASE == 96) fa_agpr_read16_96(x);
+    else if constexpr (BASE == 112) fa_agpr_read16_112(x);
+    else if constexpr (BASE == 128) fa_agpr_read16_128(x);
+    else fa_agpr_read16_144(x);
+    f32x16 v;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = x[i];
+    return v;
+}
+template <int BASE>
+__device__ __forceinline__ float agpr_read1() {
+    if constexpr (BASE == 64) return fa_agpr_read1_64();
+    else if constexpr (BASE == 80) return fa_agpr_read1_80();
+    else if constexpr (BASE == 128) return fa_agpr_read1_128();
+    else return fa_agpr_read1_144();
+}
+
+// one MFMA of S^T = K.Q^T into arch VGPRs (inline asm, so hipcc keeps it in program order among
+// the softmax slices); first: C = 0
+template <bool kF16>
+__device__ __forceinline__ void mfma_sv(const bool first, f32x16 &acc, const u32x4 &a, const u32x4 &b) {
+    if (first) {
+        if constexpr (kF16) asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "v"(b));
+        else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "v"(b));
+    } else {
+        if constexpr (kF16) asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+        else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+    }
+}
+
+// An asm-issued MFMA's result is invisible to hipcc's hazard recognizer: before the first VALU
+// read of S (or AGPR read of O) after its last MFMA, 21 wait states (32x32x16 = 16 passes).
+__device__ __forceinline__ void s_ready(f32x16 &s0, f32x16 &s1) {
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" : "+v"(s0), "+v"(s1));
+}
+__device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" ::: "memory"); }
+
+#define FA_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+
+// Opaque redefinition: ties a value to this point of the (volatile-asm ordered) instruction stream,
+// so IR-level sinking / hoisting cannot move the VALU slices out of their MFMA gap.
+__device__ __forceinline__ void pin(float &x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(u32x4 &x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(uint32_t &x) { asm volatile("" : "+v"(x)); }
+
+__device__ __forceinline__ uint32_t lds_u32(const void *ptr) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)ptr;
+}
+
+// LDS-DMA of NP 1-KiB pieces (one per wave-instruction) from rs + voff[n] to LDS lds0 + n*1024.
+// Issued from asm so hipcc does not see an LDS write it cannot disambiguate (it would otherwise
+// wait vmcnt(0) before the next ds_read of any slot); the caller retires it with an explicit
+// s_waitcnt vmcnt(0) before the tile's barrier. M0 is saved and restored around the statement.
+template <int NP>
+__device__ __forceinline__ void dma_pieces(const rsrc_t &rs, const uint32_t lds0, const int *voff) {
+    uint32_t keep;
+    if constexpr (NP == 4)
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_nop 4\n\t"
+            "s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %6, 0 offen lds\n\t"
+            "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %3, %6, 0 offen lds\n\t"
+            "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %4, %6, 0 offen lds\n\t"
+            "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %5, %6, 0 offen lds\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "s"(lds0), "v"(voff[0]), "v"(voff[1]), "v"(voff[2]), "v"(voff[3]), "s"(rs)
+            : "memory", "scc");
+    else
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_nop 4\n\t"
+            "s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %4, 0 offen lds\n\t"
+            "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %3, %4, 0 offen lds\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "s"(lds0), "v"(voff[0]), "v"(voff[1]), "s"(rs)
+            : "memory", "scc");
+}
+// one LDS-DMA piece (1 KiB per wave-instruction) from rs + voff to LDS lds; nop: 5 wait states
+// ahead of the descriptor read (a VALU write of those SGPRs is invisible to the hazard recognizer)
+__device__ __forceinline__ void dma_one(const rsrc_t &rs, const uint32_t lds, const int voff, const bool nop) {
+    uint32_t keep;
+    if (nop)
+        asm volatile("s_mov_b32 %0, m0\n\ts_nop 4\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                     "buffer_load_dwordx4 %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "s"(lds), "v"(voff), "s"(rs) : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                     "buffer_load_dwordx4 %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "s"(lds), "v"(voff), "s"(rs) : "memory");
+}
+__device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// =============================================================================================
+// fa_fwd_w4: one wave per SIMD, 64 query rows per wave (two 32-row blocks A and B). Per KV tile j:
+//
+//   P1(j): S_A(j), S_B(j) = K_j . Q^T   (32 MFMAs, K fragments shared)  ||  softmax part 2 of j-1
+//   P2(j): O += V_{j-1}^T . P^T(j-1)    (2*DTL+2 MFMAs per 16 keys: both blocks share the V^T
+//          fragments; the row sums of P ride on an extra MFMA with an all-ones A operand)
+//                                                                      ||  softmax part 1 of j
+//          then (rarely) rescale O and the row sums of a block whose max grew past the threshold
+//
+// MFMAs are inline asm (S into arch VGPRs, O and row sums into literal AGPRs, fa_agpr_asm.inc),
+// with slices of softmax VALU pinned between them (pin + sched_barrier). Operand fragments are
+// read from LDS one k-step ahead. S and P are double-buffered by tile parity (loop unrolled by
+// 2). K/V tiles arrive by LDS-DMA (asm buffer_load ... lds, 1 KiB per wave-instruction): K_{j+1}
+// and V_j are issued at the top of iteration j into 2-slot rings, with the XOR swizzle of the
+// LDS images applied on the per-lane SOURCE offsets; Q is DMA'd once. One barrier per tile.
+// Tiles that need masking (causal diagonal, Sk tail) run a non-pipelined body after the pipeline
+// has been drained.
+// =============================================================================================
+template <class DT, bool kCausal, int kD, bool kExactD>
+__global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const int n_qtiles, const int dbg) {
+    using G = Geo<kD>;
+    constexpr bool F = DT::kIsF16;
+    constexpr int KS = G::kKSteps;
+    constexpr int DTL = G::kDTiles;
+    constexpr int RB = G::kRowBytes;
+    constexpr int T = G::kTileBytes;
+    constexpr int NP = T / 4 / 1024;  // LDS-DMA pieces per wave per K or V tile (4 / 2)
+    constexpr int ROWS_PER_PIECE = 1024 / RB;
+    constexpr int LA = 32 * DTL, LB = 32 * DTL + 16;  // row-sum accumulators (AGPR bases)
+    // LDS: K slots 0,1 | V slots 0,1 | Q of the 4 waves (64 rows each). K and V sit below 64 KiB
+    // so every fragment read is a per-lane base plus a 16-bit immediate offset.
+    constexpr int KV0 = 0;
+    constexpr int QOFF = 4 * T;
+    __shared__ __attribute__((aligned(1024))) char lds[QOFF + 4 * T];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31;
+    const int h = lane >> 5;
+
+    // ---- XCD-aware work decode (as fa_fwd_w8) ------------------------------------------
+    const uint32_t nwg = gridDim.x;
+    const uint32_t bid = blockIdx.x;
+    const uint32_t xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const uint32_t w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const uint32_t t = w % (uint32_t)n_qtiles;
+    const uint32_t bh = w / (uint32_t)n_qtiles;
+    const int hq = (int)(bh % (uint32_t)p.num_heads_q);
+    const int b = (int)(bh / (uint32_t)p.num_heads_q);
+    const int qtile = kCausal ? (n_qtiles - 1 - (int)t) : (int)t;
+    const int hkv = hq / (int)p.head_q_per_group;
+
+    const int Sq = (int)p.seqlen_q, Sk = (int)p.seqlen_kv, D = (int)p.headdim;
+    const float sc = p.softmax_scale;
+    const float thr_raw = kRescaleThr / sc;
+
+    const char *qb = (const char *)p.q_ptr + 2 * ((int64_t)b * p.q_batch_stride + (int64_t)hq * p.q_head_stride);
+    const char *kb = (const char *)p.k_ptr + 2 * ((int64_t)b * p.k_batch_stride + (int64_t)hkv * p.k_head_stride);
+    const char *vb = (const char *)p.v_ptr + 2 * ((int64_t)b * p.v_batch_stride + (int64_t)hkv * p.v_head_stride);
+    char *ob = (char *)p.o_ptr + 2 * ((int64_t)b * p.o_batch_stride + (int64_t)hq * p.o_head_stride);
+
+    const int m0 = qtile * kBlockM;
+    const int mw = m0 + wave * 64;  // block A: rows mw..mw+31, block B: rows mw+32..mw+63
+    const int diag = Sk - Sq;
+
+    const int n_blocks = (Sk + kBlockN - 1) / kBlockN;
+    int n_end = n_blocks;
+    if (kCausal) {
+        const int x = diag + min(m0 + kBlockM, Sq);
+        const int nb = x <= 0 ? 0 : (x + kBlockN - 1) / kBlockN;
+        n_end = min(nb, n_blocks);
+    }
+    // leading tiles with no masked score for any row of the WORKGROUP (pipelined; the same count
+    // for all waves keeps the LDS ring and the barriers aligned)
+    int n_pipe = Sk / kBlockN;
+    if (kCausal) {
+        const int x = m0 + diag + 1;  // keys visible to the workgroup's first row
+        n_pipe = min(n_pipe, x <= 0 ? 0 : x / kBlockN);
+    }
+    n_pipe = min(n_pipe, n_end);
+    if (dbg & 1) n_pipe = 0;  // debug: every tile through the non-pipelined body
+
+    // ---- Q: this wave's 64 rows go to LDS once (LDS-DMA, K-style swizzle on the source side) --
+    const int qs = (int)p.q_seqlen_stride;
+    char *const Qw = lds + QOFF + wave * T;
+    {
+        const rsrc_t qr = make_rsrc(qb + 2 * (int64_t)mw * qs, slab_bytes(min(Sq - mw, 64), qs, D));
+        int qoff[4 * NP];
+#pragma unroll
+        for (int n = 0; n < 4 * NP; ++n) {
+            const int row = n * ROWS_PER_PIECE + (16 * lane) / RB;
+            const int slot = ((16 * lane) % RB) / 16;
+            const int ch = G::k_off(row, slot) % RB / 16;
+            qoff[n] = (kExactD || ch * 8 < D) ? row * qs * 2 + 16 * ch : 0x7ffffff0;  // past the end -> 0
+        }
+#pragma unroll
+        for (int n = 0; n < 4; ++n) dma_pieces<NP>(qr, lds_u32(Qw) + n * NP * 1024, qoff + n * NP);
+    }
+
+    // ---- LDS-DMA staging: this wave writes pieces (wave*NP + n) of each K and V tile --------
+    const int ks_ = (int)p.k_seqlen_stride, vs_ = (int)p.v_seqlen_stride;
+    int kvo[NP], vvo[NP];
+#pragma unroll
+    for (int n = 0; n < NP; ++n) {
+        const int row = (wave * NP + n) * ROWS_PER_PIECE + (16 * lane) / RB;
+        const int slot = ((16 * lane) % RB) / 16;
+        const int kch = G::k_off(row, slot) % RB / 16;  // the XOR swizzles are involutions
+        const int vch = G::v_off(row, slot) % RB / 16;
+        kvo[n] = (kExactD || kch * 8 < D) ? row * ks_ * 2 + 16 * kch : 0x7ffffff0;
+        vvo[n] = (kExactD || vch * 8 < D) ? row * vs_ * 2 + 16 * vch : 0x7ffffff0;
+    }
+    auto stage_k = [&](const int j) {
+        const int key0 = j * kBlockN;
+        const rsrc_t kr = make_rsrc(kb + 2 * (int64_t)key0 * ks_, slab_bytes(min(Sk - key0, kBlockN), ks_, D));
+        dma_pieces<NP>(kr, lds_u32(lds + KV0 + (j & 1) * T) + wave * NP * 1024, kvo);
+    };
+    auto stage_v = [&](const int j) {
+        const int key0 = j * kBlockN;
+        const rsrc_t vr = make_rsrc(vb + 2 * (int64_t)key0 * vs_, slab_bytes(min(Sk - key0, kBlockN), vs_, D));
+        dma_pieces<NP>(vr, lds_u32(lds + KV0 + (2 + (j & 1)) * T) + wave * NP * 1024, vvo);
+    };
+
+    // ---- per-lane LDS read addresses -----------------------------------------------------
+    const int g = lane >> 4;
+    const int qq = (lane >> 2) & 3;
+    const int pp = lane & 3;
+    int v_addr[DTL];
+#pragma unroll
+    for (int dt = 0; dt < DTL; ++dt)
+        v_addr[dt] = G::v_off(4 * (g >> 1) + qq, dt * 4 + 2 * (g & 1) + (pp >> 1)) + 8 * (pp & 1);
+    int k_addr[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) k_addr[ks] = G::k_off(r, 2 * ks + h);
+    // Q fragment addresses (above 64 KiB, so absolute per k-step; block B is +32 rows)
+    int q_addr[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) q_addr[ks] = (int)lds_u32(Qw) + k_addr[ks];
+    typedef __attribute__((address_space(3))) const u32x4 lds_u32x4;
+    auto qread = [&](int ks, int boff) { return *(lds_u32x4 *)(uintptr_t)(q_addr[ks] + boff); };
+    // ---- state ------------------------------------------------------------------------------
+    struct Sm {               // online-softmax state of one block (per lane: one query row)
+        float m, msc, alpha;  // running max (unscaled), m*sc, alpha of the last decision
+        float mE, mO;         // two max chains over the tile being reduced (mE then holds m_new)
+        float l, t;           // this lane's half of the row sum over finished tiles; s0 sum of the
+                              // tile being reduced (new scale, folded into l at the rescale)
+        bool resc;
+    };
+    Sm st[2];
+#pragma unroll
+    for (int X = 0; X < 2; ++X) st[X] = {kNeg, 0.f, 1.f, kNeg, kNeg, 0.f, 0.f, false};
+    f32x16 S[2][4];  // [tile parity][2 * block + half]: half 0 = keys 0-31, 1 = keys 32-63
+    u32x4 P[2][8];   // [tile parity][4 * block + k-step]
+    if constexpr (DTL == 4) fa_agpr_zero_4(); else fa_agpr_zero_2();
+
+    // ---- softmax units (each a few VALU instructions, placed between single MFMAs) ----------
+    // max chain unit i (0..15) of block X: scores i of both halves
+    auto u_max = [&](const int c, const int X, const int i) {
+        const f32x16 &s0 = S[c][2 * X], &s1 = S[c][2 * X + 1];
+        float &mm = (i & 1) ? st[X].mO : st[X].mE;
+        mm = (i < 2) ? fmaxf(s0[i], s1[i]) : fmaxf(mm, fmaxf(s0[i], s1[i]));
+        pin(mm);
+    };
+    // the rescale decision of block X in two units: the row max and m_new; then m*sc and alpha
+    auto u_dec = [&](const int X, const int k) {
+        Sm &Z = st[X];
+        if (k == 0) {
+            const float mx = pair_max(fmaxf(Z.mE, Z.mO));
+            Z.resc = __builtin_amdgcn_ballot_w64(mx > Z.m + thr_raw) != 0;
+            Z.mE = Z.resc ? fmaxf(Z.m, mx) : Z.m;
+            pin(Z.mE);
+        } else {
+            const float m_new = Z.mE;
+            const float seen = m_new > 0.5f * kNeg ? 1.f : 0.f;  // m_new * sc, or 0 before any visible key
+            const float msc_new = Z.resc ? m_new * sc * seen : Z.msc;
+            Z.alpha = __builtin_amdgcn_exp2f(Z.msc - msc_new);
+            Z.m = m_new;
+            Z.msc = msc_new;
+            pin(Z.msc);
+            pin(Z.alpha);
+        }
+    };
+    // P = exp2(s * sc - m * sc) of score v of half hf of block X, in place
+    auto u_exp = [&](const int c, const int X, const int hf, const int v) {
+        f32x16 &s = S[c][2 * X + hf];
+        float x = __builtin_amdgcn_exp2f(__builtin_fmaf(s[v], sc, -st[X].msc));
+        pin(x);
+        s[v] = x;
+    };
+    // row sum of P (half 0 -> t, half 1 -> l) and, for odd v, the rounded pair (v-1, v) into the
+    // P.V operand of its 16-key k-step
+    auto u_fin = [&](const int c, const int X, const int hf, const int v) {
+        const f32x16 &s = S[c][2 * X + hf];
+        float &acc = hf ? st[X].l : st[X].t;
+        acc = (hf == 0 && v == 0) ? s[0] : acc + s[v];
+        pin(acc);
+        if (v & 1) {
+            uint32_t w = DT::pack(s[v - 1], s[v]);
+            pin(w);
+            P[c][4 * X + 2 * hf + (v >> 3)][(v & 7) >> 1] = w;
+        }
+    };
+    auto rescale = [&]() {
+        if (st[0].resc) agpr_scale<DTL, false>(st[0].alpha);
+        if (st[1].resc) agpr_scale<DTL, true>(st[1].alpha);
+#pragma unroll
+        for (int X = 0; X < 2; ++X) st[X].l = __builtin_fmaf(st[X].l, st[X].alpha, st[X].t);
+    };
+
+    // ---- phase 1: S[c] = K.Q^T for both blocks (4*KS single MFMAs) ----------------------------
+    // gap g (after MFMA g): next k-step's K / Q fragments (gaps 4ks, 4ks+1), one LDS-DMA piece
+    // (gap 4ks+2: K_{j+1} pieces, then V_j pieces), and with SM2 the second softmax half of the
+    // tile of parity pr (32 units: block u&1, score u>>1 of half 1).
+    constexpr int G1 = 4 * KS;
+    auto phase1 = [&](const char *K, auto PAR, auto SM2, auto DMA, const rsrc_t &kr, const rsrc_t &vr,
+                      const uint32_t k_lds, const uint32_t v_lds) {
+        constexpr int c = decltype(PAR)::value, pr = c ^ 1;
+        constexpr bool do_sm = decltype(SM2)::value, do_dma = decltype(DMA)::value;
+        u32x4 kf[2][2], qf[2][2];  // [buffer][key half | block]
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+            kf[0][x] = *(const u32x4 *)(K + x * 32 * RB + k_addr[0]);
+            qf[0][x] = qread(0, x * 32 * RB);
+        }
+        static_for<G1>([&](auto G) {
+            constexpr int g = decltype(G)::value;
+            constexpr int ks = g >> 2, i = g & 3, cb = ks & 1;
+            mfma_sv<F>(ks == 0, S[c][i], kf[cb][i & 1], qf[cb][i >> 1]);
+            if constexpr (ks + 1 < KS && i < 2) {
+                kf[cb ^ 1][i] = *(const u32x4 *)(K + i * 32 * RB + k_addr[ks + 1]);
+                qf[cb ^ 1][i] = qread(ks + 1, i * 32 * RB);
+            }
+            if constexpr (do_dma && i == 2) {
+                if constexpr (ks < NP) dma_one(kr, k_lds + ks * 1024, kvo[ks], ks == 0);
+                else dma_one(vr, v_lds + (ks - NP) * 1024, vvo[ks - NP], ks == NP);
+            }
+            if constexpr (do_sm) {
+                static_for<32>([&](auto U) {
+                    constexpr int u = decltype(U)::value;
+                    if constexpr ((u * G1) / 32 == g) {
+                        u_exp(pr, u & 1, 1, u >> 1);
+                        if constexpr (u >= 2) u_fin(pr, u & 1, 1, (u >> 1) - 1);
+                    }
+                });
+            }
+            FA_SCHED_FENCE();
+        });
+        if constexpr (do_sm) {
+            u_fin(pr, 0, 1, 15);
+            u_fin(pr, 1, 1, 15);
+        }
+    };
+    // the same second softmax half without MFMAs (drain and masked tiles)
+    auto sm2_all = [&](auto PAR) {
+        constexpr int c = decltype(PAR)::value;
+        static_for<16>([&](auto VV) {
+            constexpr int v = decltype(VV)::value;
+            static_for<2>([&](auto XX) {
+                u_exp(c, decltype(XX)::value, 1, v);
+                u_fin(c, decltype(XX)::value, 1, v);
+            });
+        });
+    };
+
+    // ---- phase 2: O^T += V^T.P^T for both blocks (8*DTL single MFMAs into the AGPRs) ----------
+    // gap g (kk = g / 2DTL, i = g % 2DTL; MFMA: block i / DTL, d-tile i % DTL): V^T read i of
+    // k-step kk+1, and with SM1 the first softmax half of the tile of parity cs (schedule below).
+    constexpr int G2 = 8 * DTL;
+    constexpr int GQ = G2 / 8;  // 4 (D=128) / 2 (D=64)
+    // exp unit e (0..31) -> block / score: A0..A4, then B and A alternating, then B11..B15
+    struct Ex {  // exp unit e (0..31) -> block / score: A0..A4, then B and A alternating, then B11..B15
+        static constexpr int blk(int e) { return e < 5 ? 0 : (e < 27 ? (((e - 5) & 1) ? 0 : 1) : 1); }
+        static constexpr int v(int e) {
+            return e < 5 ? e : (e < 27 ? (((e - 5) & 1) ? 5 + ((e - 5) >> 1) : (e - 5) >> 1) : 11 + (e - 27));
+        }
+        static constexpr int gap(int e) { return GQ + 2 + (e * (G2 - GQ - 2)) / 32; }
+        static constexpr int max_gap(int X, int m) { return X * GQ + (m * GQ) / 16; }
+        static constexpr int dec_gap(int X, int k) { return (X + 1) * GQ + (GQ == 2 ? 0 : k); }
+    };
+    static_assert([] {  // the schedule respects max -> decision -> exp of each block, and fits
+        for (int X = 0; X < 2; ++X) {
+            if (Ex::dec_gap(X, 0) < Ex::max_gap(X, 15) || Ex::dec_gap(X, 1) < Ex::dec_gap(X, 0)) return false;
+            if (Ex::max_gap(X, 15) >= G2) return false;
+        }
+        for (int e = 0; e < 32; ++e) {
+            if (Ex::gap(e) < Ex::dec_gap(Ex::blk(e), 1) || Ex::gap(e) >= G2) return false;
+            if (e > 0 && Ex::gap(e) < Ex::gap(e - 1)) return false;
+        }
+        return true;
+    }(), "phase-2 softmax schedule");
+    auto phase2 = [&](const char *V, auto PPV, auto PSM, auto SM1) {
+        constexpr int cp = decltype(PPV)::value, cs = decltype(PSM)::value;
+        constexpr bool do_sm = decltype(SM1)::value;
+        u32x4 va[2][DTL];
+        auto rd = [&](const int kk, const int n, u32x4 *dst) {
+            const int rowoff = ((kk >> 1) * 32 + (kk & 1) * 16) * RB + (n & 1) * 8 * RB;
+            const u32x2 x = tr_read(V + rowoff + v_addr[n >> 1]);
+            dst[n >> 1][2 * (n & 1)] = x[0];
+            dst[n >> 1][2 * (n & 1) + 1] = x[1];
+        };
+#pragma unroll
+        for (int n = 0; n < 2 * DTL; ++n) rd(0, n, va[0]);
+        static_for<G2>([&](auto G) {
+            constexpr int g = decltype(G)::value;
+            constexpr int kk = g / (2 * DTL), i = g % (2 * DTL), X = i / DTL, dt = i % DTL;
+            agpr_mfma<F, X * 16 * DTL + 16 * dt>(va[kk & 1][dt], P[cp][4 * X + kk]);
+            if constexpr (kk + 1 < 4) rd(kk + 1, i, va[(kk + 1) & 1]);
+            if constexpr (do_sm) {
+                static_for<32>([&](auto M) {
+                    constexpr int X2 = decltype(M)::value >> 4, m = decltype(M)::value & 15;
+                    if constexpr (Ex::max_gap(X2, m) == g) u_max(cs, X2, m);
+                });
+                static_for<4>([&](auto K2) {
+                    constexpr int X2 = decltype(K2)::value >> 1, k = decltype(K2)::value & 1;
+                    if constexpr (Ex::dec_gap(X2, k) == g) u_dec(X2, k);
+                });
+                static_for<32>([&](auto E) {
+                    constexpr int e = decltype(E)::value;
+                    if constexpr (Ex::gap(e) + 1 == g) u_fin(cs, Ex::blk(e), 0, Ex::v(e));
+                    if constexpr (Ex::gap(e) == g) u_exp(cs, Ex::blk(e), 0, Ex::v(e));
+                });
+            }
+            FA_SCHED_FENCE();
+        });
+        if constexpr (do_sm) {
+            static_for<32>([&](auto E) {
+                constexpr int e = decltype(E)::value;
+                if constexpr (Ex::gap(e) == G2 - 1) u_fin(cs, Ex::blk(e), 0, Ex::v(e));
+            });
+        }
+    };
+    // the same first softmax half without MFMAs (masked tiles)
+    auto sm1_all = [&](auto PAR) {
+        constexpr int c = decltype(PAR)::value;
+        static_for<2>([&](auto XX) {
+            constexpr int X = decltype(XX)::value;
+            static_for<16>([&](auto M) { u_max(c, X, decltype(M)::value); });
+            u_dec(X, 0);
+            u_dec(X, 1);
+            static_for<16>([&](auto VV) {
+                u_exp(c, X, 0, decltype(VV)::value);
+                u_fin(c, X, 0, decltype(VV)::value);
+            });
+        });
+    };
+
+    auto k_rsrc = [&](const int j) {
+        const int key0 = j * kBlockN;
+        return make_rsrc(kb + 2 * (int64_t)key0 * ks_, slab_bytes(min(Sk - key0, kBlockN), ks_, D));
+    };
+    auto v_rsrc = [&](const int j) {
+        const int key0 = j * kBlockN;
+        return make_rsrc(vb + 2 * (int64_t)key0 * vs_, slab_bytes(min(Sk - key0, kBlockN), vs_, D));
+    };
+    const uint32_t lds_base = lds_u32(lds) + wave * NP * 1024;  // this wave's pieces of slot 0
+
+    // ---- prologue -------------------------------------------------------------------------
+    // tile -1 of the pipeline is empty: its S = kNeg gives P = 0, and its P.V reads V slot 1,
+    // zeroed here so that 0 * V stays 0.
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        S[1][1][i] = kNeg;
+        S[1][3][i] = kNeg;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) P[1][i] = (u32x4){0, 0, 0, 0};
+    {
+        constexpr int per_thread = T / 256 / 16;
+#pragma unroll
+        for (int i = 0; i < per_thread; ++i) *(u32x4 *)(lds + KV0 + 3 * T + (i * 256 + tid) * 16) = (u32x4){0, 0, 0, 0};
+    }
+    if (n_end > 0) stage_k(0);
+    dma_wait();       // Q and K_0 landed
+    __syncthreads();  // visible to every wave
+
+    // ---- pipelined tiles: iteration j = P1(S_j || softmax half 2 of j-1, DMA K_{j+1}, V_j),
+    //      P2(O += P_{j-1} V_{j-1} || softmax half 1 of j), rescale, barrier -------------------
+    auto iter = [&](const int j, auto PAR) {
+        constexpr int c = decltype(PAR)::value, pr = c ^ 1;
+        const rsrc_t kr = k_rsrc(j + 1), vr = v_rsrc(j);
+        phase1(lds + KV0 + c * T, PAR, IC<1>{}, IC<1>{}, kr, vr, lds_base + pr * T, lds_base + (2 + c) * T);
+        phase2(lds + KV0 + (2 + pr) * T, IC<pr>{}, PAR, IC<1>{});
+        rescale();
+        dma_wait();  // K_{j+1}, V_j landed
+        __syncthreads();
+    };
+    for (int j = 0; j < n_pipe; j += 2) {
+        iter(j, IC<0>{});
+        if (j + 1 < n_pipe) iter(j + 1, IC<1>{});
+    }
+    // drain the last pipelined tile: softmax half 2 and P.V
+    auto drain = [&](auto PAR) {
+        constexpr int c = decltype(PAR)::value;
+        sm2_all(PAR);
+        phase2(lds + KV0 + (2 + c) * T, PAR, PAR, IC<0>{});
+    };
+    if (n_pipe > 0) {
+        if ((n_pipe - 1) & 1) drain(IC<1>{}); else drain(IC<0>{});
+    }
+
+    // ---- remaining tiles: masked, not pipelined --------------------------------------------
+    if (n_pipe < n_end) {
+        stage_v(n_pipe);  // the pipeline fetched V one tile late; catch up before the first one
+        dma_wait();
+        __syncthreads();
+    }
+    for (int j = n_pipe; j < n_end; ++j) {
+        if (j + 1 < n_end) {
+            stage_k(j + 1);
+            stage_v(j + 1);
+        }
+        const char *K = lds + KV0 + (j & 1) * T;
+        const char *V = lds + KV0 + (2 + (j & 1)) * T;
+        const int key0 = j * kBlockN;
+        phase1(K, IC<0>{}, IC<0>{}, IC<0>{}, k_rsrc(j), k_rsrc(j), 0u, 0u);
+        s_ready(S[0][0], S[0][1]);
+        s_ready(S[0][2], S[0][3]);
+        auto mask = [&](f32x16 &s0, f32x16 &s1, const int row) {
+            const int lim = kCausal ? min(Sk - 1, row + diag) : Sk - 1;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int kk = key0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                if (kk > lim) s0[i] = kNeg;
+                if (kk + 32 > lim) s1[i] = kNeg;
+            }
+        };
+        mask(S[0][0], S[0][1], mw + r);
+        mask(S[0][2], S[0][3], mw + 32 + r);
+        sm1_all(IC<0>{});
+        rescale();
+        sm2_all(IC<0>{});
+        phase2(V, IC<0>{}, IC<0>{}, IC<0>{});
+        dma_wait();
+        __syncthreads();
+    }
+
+    // ---- epilogue ---------------------------------------------------------------------------
+    mfma_drain();  // last asm MFMA -> AGPR reads
+    const int os_ = (int)p.o_seqlen_stride;
+    const rsrc_t orr = make_rsrc(ob + 2 * (int64_t)mw * os_, slab_bytes(min(Sq - mw, 64), os_, D));
+    auto store_block = [&](const int row, auto OBASE, const float l_lane) {
+        constexpr int ob0 = decltype(OBASE)::value;
+        f32x16 o[DTL];
+        o[0] = agpr_read16<ob0>();
+        o[1] = agpr_read16<ob0 + 16>();
+        if constexpr (DTL == 4) {
+            o[2] = agpr_read16<ob0 + 32>();
+            o[3] = agpr_read16<ob0 + 48>();
+        }
+        const float l_tot = pair_sum(l_lane);
+        const float inv = (l_tot == 0.f) ? 1.f : 1.f / l_tot;
+        const int orow = row * os_ * 2;
+#pragma unroll
+        for (int dt = 0; dt < DTL; ++dt) {
+#pragma unroll
+            for (int gp = 0; gp < 4; gp += 2) {
+                const uint32_t a0 = DT::pack(o[dt][4 * gp + 0] * inv, o[dt][4 * gp + 1] * inv);
+                const uint32_t a1 = DT::pack(o[dt][4 * gp + 2] * inv, o[dt][4 * gp + 3] * inv);
+                const uint32_t b0 = DT::pack(o[dt][4 * gp + 4] * inv, o[dt][4 * gp + 5] * inv);
+                const uint32_t b1 = DT::pack(o[dt][4 * gp + 6] * inv, o[dt][4 * gp + 7] * inv);
+                const auto x0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+                const auto x1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+                const int d0 = dt * 32 + 8 * (gp + h);
+                if (kExactD || d0 < D)
+                    __builtin_amdgcn_raw_buffer_store_b128((u32x4){x0[0], x1[0], x0[1], x1[1]}, orr, orow + 2 * d0, 0,
+                                                           0);
+            }
+        }
+    };
+    store_block(r, IC<0>{}, st[0].l);
+    store_block(r + 32, IC<16 * DTL>{}, st[1].l);
+}
+
+// ---- host launch of one instantiation -------------------------------------------------
+template <class DT, bool C, int kD, bool kExact>
+int launch_one(const fa_fwd_params &p, hipStream_t stream) {
+    const int64_t n_qtiles = (p.seqlen_q + kBlockM - 1) / kBlockM;
+    const int64_t nwg = n_qtiles * p.num_heads_q * p.batch_size;
+    const int variant = variant_from_env();
+    if (variant == 1)
+        hipLaunchKernelGGL((fa_fwd_w8<DT, C, kD, kExact>), dim3((uint32_t)nwg), dim3(kThreads), 0, stream, p,
+                           (int)n_qtiles);
+    else
+        hipLaunchKernelGGL((fa_fwd_w4<DT, C, kD, kExact>), dim3((uint32_t)nwg), dim3(256), 0, stream, p,
+                           (int)n_qtiles, variant == 2 ? 1 : 0);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "HIP launch failed: %s", hipGetErrorString(e));
+    return FA_OK;
+}
+
+}  // namespace fa

@@ -19,8 +19,8 @@ _lib = None
 def build(force: bool = False) -> Path:
     src = HERE / "fa_oracle.c"
     if force or not LIB.exists() or LIB.stat().st_mtime < src.stat().st_mtime:
-        subprocess.run(["make", "-C", str(HERE), "-s", "-B" if force else ""], check=True,
-                       capture_output=True)
+        cmd = ["make", "-C", str(HERE), "-s"] + (["-B"] if force else [])
+        subprocess.run(cmd, check=True, capture_output=True)
     return LIB
 
 

@@ -1,0 +1,33 @@
+"""Turn a scripts/profile.sh (or pmc.sh) output dir into profiles/pmc_<config>.json.
+
+HBM traffic per launch of the attention kernel, corrected as MI355X_MICROARCH.md 'HBM' prescribes:
+FETCH_SIZE and WRITE_SIZE are kilobytes; on gfx950 FETCH_SIZE reports half the bytes of a wide
+(16 B / lane) streaming read, so it is doubled; WRITE_SIZE is exact for 16 B / lane stores.
+usage: python scripts/pmc_to_json.py <prof dir> <config> <out json> [source note]
+"""
+import collections
+import csv
+import glob
+import json
+import sys
+
+src, cfg, out = sys.argv[1], sys.argv[2], sys.argv[3]
+note = sys.argv[4] if len(sys.argv) > 4 else src
+agg = collections.defaultdict(list)
+for f in glob.glob(f"{src}/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        if "fa::fa_fwd" in r["Kernel_Name"]:
+            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+mean = {k: sum(v) / len(v) for k, v in agg.items()}
+res = {"config": cfg, "source": note, "dispatches": {k: len(v) for k, v in agg.items()},
+       "counters_mean_per_dispatch": mean}
+if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
+    fetch = mean["FETCH_SIZE"] * 1024 * 2
+    write = mean["WRITE_SIZE"] * 1024
+    res.update({"fetch_bytes_corrected": fetch, "write_bytes": write, "hbm_bytes_per_launch": fetch + write})
+if "GRBM_GUI_ACTIVE" in mean:
+    res["xcd_active_cycles"] = mean["GRBM_GUI_ACTIVE"] / 8
+if "SQ_VALU_MFMA_BUSY_CYCLES" in mean and "GRBM_GUI_ACTIVE" in mean:
+    res["mfma_busy_frac"] = mean["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / (mean["GRBM_GUI_ACTIVE"] / 8)
+json.dump(res, open(out, "w"), indent=1)
+print(json.dumps(res, indent=1))

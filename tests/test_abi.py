@@ -124,5 +124,5 @@ def test_geometry(lib):
     rc = lib.fa_fwd_gfx950_geometry(ctypes.byref(good_params()), 0, *[ctypes.byref(x) for x in vals])
     assert rc == FA_OK
     bm, bn, thr, wg = (x.value for x in vals)
-    assert (bm, bn, thr) == (256, 64, 512)
+    assert (bm, bn, thr) == (256, 64, 256)  # fa_fwd_w4: 4 waves
     assert wg == 2 * 8 * ((300 + bm - 1) // bm)
