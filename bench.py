@@ -6,7 +6,7 @@ Metric (BASELINE.json): attn fwd TFLOPS + %MFMA peak at (B,H,S,D) = (4,32,4096,1
 ``flash_attn_func`` (custom op -> C++ host API -> C-ABI -> HIP kernel) over one batch of
 synthetic N(0,1) q, k, v already resident in HBM.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|decode]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|decode]
 
 Multi-GPU (launched by torch.distributed.run, one process per GPU): every rank runs the full
 workload on its own seeded shard of batch x heads (weak scaling; attention tiles are independent,
@@ -45,6 +45,10 @@ CONFIGS = {
                D=128, dtype="bf16", causal=True),
     "c4": dict(workload="C4 GQA fp16 B4 Hq32 Hkv8 S4096 D128 causal", B=4, Hq=32, Hkv=8, Sq=4096,
                Sk=4096, D=128, dtype="fp16", causal=True),
+    # C5: Llama-3-8B attention (Hq32 Hkv8 D128), bf16 causal prefill S4096; global batch 8 sharded
+    # over (batch, kv-head) units -- one batch row per GPU at N=8 (flash_attention_cute_amd/shard.py)
+    "c5": dict(workload="C5 Llama-3-8B attn bf16 causal B1(per GPU) Hq32 Hkv8 S4096 D128", B=1, Hq=32, Hkv=8,
+               Sq=4096, Sk=4096, D=128, dtype="bf16", causal=True),
     "decode": dict(workload="decode GQA fp16 B32 Hq32 Hkv8 Sq1 Sk4096 D128 (q-head pack)", B=32, Hq=32,
                    Hkv=8, Sq=1, Sk=4096, D=128, dtype="fp16", causal=False),
 }
@@ -126,6 +130,32 @@ def load_traffic(config_key: str):
         return None
 
 
+def roofline(c, kern_ms: float, traffic):
+    """Roofline of the attention kernel: MFMA-bound for prefill (intensity ~2 kFLOP/B at S=4096),
+    HBM-bound for decode (Sq = 1: one pass over K/V per q-head group)."""
+    gbs = algo_bytes(c) / (kern_ms * 1e-3) / 1e9
+    tf = flops(c) / (kern_ms * 1e-3) / 1e12
+    base = {"traffic": traffic, "kernel_ms": round(kern_ms, 4), "algorithmic_bytes": algo_bytes(c),
+            "algorithmic_flops": flops(c)}
+    if c["Sq"] == 1:
+        return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(gbs / HBM_PEAK_GBS, 4), "achieved_TFLOPs": round(tf, 3), **base}
+    return {"bound": "mfma", "achieved": round(tf, 3), "peak": PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / PEAK_TFLOPS, 4), "algorithmic_GBs": round(gbs, 1), **base}
+
+
+def reduce_max(world: int, *vals: float):
+    """Max over ranks of host-side timings (gloo, CPU tensor): the harness's only cross-rank traffic."""
+    if world <= 1:
+        return vals
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor(vals, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return tuple(float(x) for x in t)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
@@ -137,6 +167,14 @@ def main() -> None:
     ap.add_argument("--seed", type=int, default=0)
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # not started by torch.distributed.run: start it as a child (never exec) and pass its status on
+        import subprocess
+
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr=127.0.0.1", f"--master-port={29500 + os.getpid() % 1000}", __file__, *sys.argv[1:]]
+        sys.exit(subprocess.call(cmd))
+
     import torch
     import torch.distributed as dist
 
@@ -146,7 +184,7 @@ def main() -> None:
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    n_gpus = world if world > 1 else args.gpus
+    n_gpus = world
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
@@ -181,14 +219,10 @@ def main() -> None:
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
 
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+    elapsed, kern_ms = reduce_max(world, elapsed, kern_ms)
 
     f_step = flops(c)
     value = n_gpus * f_step * args.steps / elapsed / 1e12
-    achieved = f_step / (kern_ms * 1e-3) / 1e12
     result = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -206,10 +240,7 @@ def main() -> None:
                    "seqlen_q": c["Sq"], "seqlen_kv": c["Sk"], "headdim": c["D"], "causal": c["causal"],
                    "parallelism": f"dp{n_gpus} (independent batch x head shard per GPU, no collective)"},
         "pct_mfma_peak": round(100.0 * value / n_gpus / PEAK_TFLOPS, 2),
-        "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / PEAK_TFLOPS, 4), "traffic": load_traffic(args.config),
-                     "kernel_ms": round(kern_ms, 4), "algorithmic_bytes": algo_bytes(c),
-                     "algorithmic_GBs": round(algo_bytes(c) / (kern_ms * 1e-3) / 1e9, 1)},
+        "roofline": roofline(c, kern_ms, load_traffic(args.config)),
         "cpu_baseline": None,
     }
     if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:

@@ -1,0 +1,108 @@
+"""Drop-in HF attention ``forward`` that routes the attention core through ``flash_attn_func``.
+
+Mirror of reference models/rope_attn_fwd.py:1-120 (the caller of the hot path),
+kept call-site identical -- q/k/v projections viewed as strided [B, H, S, D] (seq stride H*D), RoPE,
+KV-cache update, ``flash_attn_func(q, k, v, causal=module.is_causal, softmax_scale=self.scaling)``,
+``transpose(1, 2)``, ``reshape(...).contiguous()``, ``o_proj`` -- with the three defects SURVEY.md 3.2
+verified against the installed transformers fixed:
+
+1. ``self.config.use_sliding_window`` raised AttributeError on ``LlamaConfig``
+   (reference models/rope_attn_fwd.py:97): read with ``getattr(..., False)``; a sliding window
+   that would actually cut the visible keys raises NotImplementedError instead of being ignored
+   (the kernel has no local-window mask);
+2. HF passes the cache as ``past_key_values=`` (plural) while the reference takes
+   ``past_key_value`` (:71) and silently drops the cache on decode: both names are accepted;
+3. decode (Sq == 1) with ``is_causal=True`` must see every cached key: the GPU kernel's causal mask
+   is bottom-right aligned (key n visible to query m iff n <= m + Sk - Sq) and the host API drops
+   the causal flag for Sq == 1 (reference csrc/flash_attention_api.cpp:81), but the op's CPU
+   default (torch SDPA, top-left) would let the query see only key 0 -- so the flag is passed as
+   ``module.is_causal and Sq > 1``, which is the same computation on the GPU and correct on CPU.
+
+Because the op's output inherits q's strides (reference csrc/flash_attention_api.cpp:85, kept in
+csrc/flash_attention_api.cpp), ``attn.transpose(1, 2).reshape(B, S, -1)`` is copy-free.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+from torch import nn
+
+from .flash_attention import flash_attn_func
+
+
+def rotate_half(x: torch.Tensor) -> torch.Tensor:
+    """[x1, x2] -> [-x2, x1] over the last dim (reference models/rope_attn_fwd.py:8-12)."""
+    half = x.shape[-1] // 2
+    return torch.cat((-x[..., half:], x[..., :half]), dim=-1)
+
+
+def apply_rotary_pos_emb(q, k, cos, sin, position_ids=None, unsqueeze_dim=1):
+    """RoPE on q [B,Hq,S,D] and k [B,Hkv,S,D] (reference models/rope_attn_fwd.py:14-38).
+
+    Elementwise on the strided projection views, so the outputs keep the [B,S,H,D] physical layout.
+    """
+    cos = cos.unsqueeze(unsqueeze_dim)
+    sin = sin.unsqueeze(unsqueeze_dim)
+    return q * cos + rotate_half(q) * sin, k * cos + rotate_half(k) * sin
+
+
+def _flash_attention_forward(module: nn.Module, query: torch.Tensor, key: torch.Tensor, value: torch.Tensor,
+                             attention_mask: Optional[torch.Tensor], dropout: float = 0.0,
+                             scaling: Optional[float] = None, sliding_window: Optional[int] = None,
+                             softcap: Optional[float] = None, **kwargs) -> Tuple[torch.Tensor, None]:
+    """Attention core (reference models/rope_attn_fwd.py:40-64): returns [B, Sq, Hq, D], None."""
+    kwargs.pop("is_causal", None)
+    if softcap is not None:
+        raise NotImplementedError("flash_attention_cute_amd: attention logit softcapping is not supported")
+    if dropout:
+        raise NotImplementedError("flash_attention_cute_amd: attention dropout is not supported (forward only)")
+    sq, sk = query.shape[2], key.shape[2]
+    if sliding_window is not None and sk > sliding_window:
+        raise NotImplementedError(
+            f"flash_attention_cute_amd: sliding window {sliding_window} shorter than the {sk} visible keys")
+    causal = bool(getattr(module, "is_causal", True)) and sq > 1
+    attn_output = flash_attn_func(query, key, value, causal=causal, softmax_scale=scaling)
+    return attn_output.transpose(1, 2), None
+
+
+def attention_forward(self: nn.Module, hidden_states: torch.Tensor,
+                      position_embeddings: Tuple[torch.Tensor, torch.Tensor],
+                      attention_mask: Optional[torch.Tensor] = None, past_key_value=None,
+                      cache_position: Optional[torch.LongTensor] = None, **kwargs):
+    """Replacement for ``LlamaAttention.forward`` / ``Qwen2Attention.forward``
+    (reference models/rope_attn_fwd.py:66-120)."""
+    cache = kwargs.pop("past_key_values", None)
+    if cache is None:
+        cache = past_key_value
+    input_shape = hidden_states.shape[:-1]
+    hidden_shape = (*input_shape, -1, self.head_dim)
+
+    # strided [B, H, S, D] views of the projections (seq stride H * D); no copies
+    query_states = self.q_proj(hidden_states).view(hidden_shape).transpose(1, 2)
+    key_states = self.k_proj(hidden_states).view(hidden_shape).transpose(1, 2)
+    value_states = self.v_proj(hidden_states).view(hidden_shape).transpose(1, 2)
+
+    cos, sin = position_embeddings
+    query_states, key_states = apply_rotary_pos_emb(query_states, key_states, cos, sin)
+
+    if cache is not None:
+        cache_kwargs = {"sin": sin, "cos": cos, "cache_position": cache_position}
+        key_states, value_states = cache.update(key_states, value_states, self.layer_idx, cache_kwargs)
+
+    cfg = self.config
+    sliding_window = None
+    if (getattr(cfg, "use_sliding_window", False) and getattr(cfg, "sliding_window", None) is not None
+            and self.layer_idx >= getattr(cfg, "max_window_layers", 0)):
+        sliding_window = cfg.sliding_window
+    elif getattr(self, "sliding_window", None) is not None:
+        sliding_window = self.sliding_window
+
+    attn_output, attn_weights = _flash_attention_forward(
+        self, query_states, key_states, value_states, attention_mask,
+        dropout=0.0 if not self.training else self.attention_dropout, scaling=self.scaling,
+        sliding_window=sliding_window, **kwargs)
+
+    attn_output = attn_output.reshape(*input_shape, -1).contiguous()
+    attn_output = self.o_proj(attn_output)
+    return attn_output, attn_weights
