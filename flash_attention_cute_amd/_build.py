@@ -73,7 +73,7 @@ def _jobs() -> int:
     return max(1, min(int(n), 16))
 
 
-def build_abi(force: bool = False, verbose: bool = False) -> Path:
+def build_abi(force: bool = False, verbose: bool = False, stamps: bool = False) -> Path:
     """Compile the HIP kernels + C-ABI into lib/libfa_gfx950.so (gfx950 code objects).
 
     Each kernel instantiation is its own translation unit (csrc/fa_inst.hip with -D selectors), so
@@ -81,30 +81,32 @@ def build_abi(force: bool = False, verbose: bool = False) -> Path:
     """
     from concurrent.futures import ThreadPoolExecutor
 
-    LIBDIR.mkdir(exist_ok=True)
-    if not force and not _stale(ABI_LIB, abi_sources()):
-        return ABI_LIB
+    out_lib = ROOT / "build" / "stamps" / "libfa_gfx950.so" if stamps else ABI_LIB
+    out_lib.parent.mkdir(parents=True, exist_ok=True)
+    if not force and not _stale(out_lib, abi_sources()):
+        return out_lib
     if not HIPCC.exists():
         raise RuntimeError(f"hipcc not found at {HIPCC}")
-    objdir = ROOT / "build" / "obj"
+    objdir = ROOT / "build" / ("obj_stamps" if stamps else "obj")
+    extra = ["-DFA_STAMPS=1"] if stamps else []
     objdir.mkdir(parents=True, exist_ok=True)
     cmds = []
     objs = []
     for dt, c, d, e in INSTANCES:
         obj = objdir / f"fa_inst_{dt.lower()}_c{c}_d{d}_x{e}.o"
         objs.append(obj)
-        cmds.append([HIPCC, *HIP_FLAGS, f"-I{INCLUDE}", f"-I{CSRC}", f"-DFA_INST_DT={dt}", f"-DFA_INST_CAUSAL={c}",
+        cmds.append([HIPCC, *HIP_FLAGS, *extra, f"-I{INCLUDE}", f"-I{CSRC}", f"-DFA_INST_DT={dt}", f"-DFA_INST_CAUSAL={c}",
                      f"-DFA_INST_D={d}", f"-DFA_INST_EXACT={e}", "-c", CSRC / "fa_inst.hip", "-o", obj])
     disp = objdir / "fa_fwd_gfx950.o"
     objs.append(disp)
-    cmds.append([HIPCC, *HIP_FLAGS, f"-I{INCLUDE}", f"-I{CSRC}", "-c", CSRC / "fa_fwd_gfx950.hip", "-o", disp])
+    cmds.append([HIPCC, *HIP_FLAGS, *extra, f"-I{INCLUDE}", f"-I{CSRC}", "-c", CSRC / "fa_fwd_gfx950.hip", "-o", disp])
     with ThreadPoolExecutor(max_workers=_jobs()) as ex:
         for f in [ex.submit(_run, cmd, verbose) for cmd in cmds]:
             f.result()
-    tmp = ABI_LIB.with_suffix(".so.tmp")
+    tmp = out_lib.with_suffix(".so.tmp")
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp], verbose)
-    os.replace(tmp, ABI_LIB)
-    return ABI_LIB
+    os.replace(tmp, out_lib)
+    return out_lib
 
 
 def build_ext(force: bool = False, verbose: bool = False) -> Path:

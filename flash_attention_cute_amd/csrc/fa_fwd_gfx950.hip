@@ -30,6 +30,16 @@ int fa::set_err(int code, const char *fmt, ...) {
 }
 
 namespace {
+unsigned long long *g_stamps = nullptr;
+}  // namespace
+
+unsigned long long *fa::stamp_buffer() { return g_stamps; }
+
+// Diagnostic hook (not in include/fa_gfx950.h): device buffer of 12 u64 per wave of the next
+// launches; honoured only by a -DFA_STAMPS=1 build of the kernels (scripts/stamps.py).
+extern "C" void fa_debug_set_stamps(void *device_buffer) { g_stamps = (unsigned long long *)device_buffer; }
+
+namespace {
 using fa::set_err;
 using fa::launch_one;
 

@@ -158,6 +158,55 @@ __device__ __forceinline__ uint32_t slab_bytes(int rows, int stride, int D) {
     return rows <= 0 ? 0u : (uint32_t)(((rows - 1) * stride + D) * 2);
 }
 
+// XCD-aware work decode. Workgroups are dealt round-robin over the 8 XCDs (blocks b and b+8 share
+// one, MI355X_MICROARCH "Workgroup dispatch"), and an XCD starts its blocks in bid order. Each XCD is
+// given a contiguous range of the logical order (batch, q-head, q-tile) -- the q-tiles of one
+// (batch, head), and the q-heads of one kv group, share that XCD's 4 MiB L2 for their K/V stream.
+// Causal: when the XCD's range is made of whole (batch, head) rows, it is cut into groups of hg
+// heads (about 64 workgroups, two per CU of the XCD; with 16 q-tiles that is 4 heads, one GQA group
+// of Llama-3) and each group is walked q-tile-major, heaviest q-tile level first across its heads
+// (longest-processing-time-first, so each group ends on light tiles while the next group's heavy
+// tiles fill the CUs that free up), keeping only hg heads' K/V in flight per XCD; otherwise each
+// (batch, head) row is walked heavy-first.
+// Bijective for any grid size; speed only, never correctness.
+#ifdef FA_STAMPS
+__device__ __forceinline__ unsigned long long xcc_id() {
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    return (unsigned long long)(x & 15);
+}
+#endif
+
+struct Work {
+    int qtile, hq, b;
+};
+template <bool kCausal>
+__device__ __forceinline__ Work decode_work(const uint32_t nwg, const uint32_t bid, const int n_qtiles, const int Hq) {
+    const uint32_t xcd = bid & 7, k = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+    const uint32_t start = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+    const uint32_t cnt = q8 + (xcd < r8 ? 1u : 0u);
+    const uint32_t nq = (uint32_t)n_qtiles;
+    uint32_t t, bh;
+    if (kCausal && start % nq == 0 && cnt % nq == 0) {
+        const uint32_t nb = cnt / nq;  // heads of this XCD
+        uint32_t hg = 64u / nq;
+        hg = hg < 1u ? 1u : (hg > nb ? nb : hg);
+        while (nb % hg) --hg;
+        const uint32_t grp = k / (hg * nq), kk = k % (hg * nq);
+        t = kk / hg;
+        bh = start / nq + grp * hg + kk % hg;
+    } else {
+        const uint32_t w = start + k;
+        t = w % nq;
+        bh = w / nq;
+    }
+    Work r;
+    r.hq = (int)(bh % (uint32_t)Hq);
+    r.b = (int)(bh / (uint32_t)Hq);
+    r.qtile = kCausal ? (n_qtiles - 1 - (int)t) : (int)t;  // causal: heavy tiles first
+    return r;
+}
+
 template <class DT, bool kCausal, int kD, bool kExactD>
 __global__ __launch_bounds__(kThreads) void fa_fwd_w8(const fa_fwd_params p, const int n_qtiles) {
     using G = Geo<kD>;
@@ -170,18 +219,8 @@ __global__ __launch_bounds__(kThreads) void fa_fwd_w8(const fa_fwd_params p, con
     const int h = lane >> 5;
 
     // ---- XCD-aware work decode ----------------------------------------------------------
-    // Blocks are dealt round-robin over the 8 XCDs (b and b+8 share one). Remap so that each
-    // XCD walks a contiguous range of the logical order (bijective for any grid size).
-    const uint32_t nwg = gridDim.x;
-    const uint32_t bid = blockIdx.x;
-    const uint32_t xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const uint32_t w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-    // logical order: batch, q-head (members of one kv group adjacent), q-tile
-    const uint32_t t = w % (uint32_t)n_qtiles;
-    const uint32_t bh = w / (uint32_t)n_qtiles;
-    const int hq = (int)(bh % (uint32_t)p.num_heads_q);
-    const int b = (int)(bh / (uint32_t)p.num_heads_q);
-    const int qtile = kCausal ? (n_qtiles - 1 - (int)t) : (int)t;  // heavy tiles first
+    const Work wk = decode_work<kCausal>(gridDim.x, blockIdx.x, n_qtiles, (int)p.num_heads_q);
+    const int hq = wk.hq, b = wk.b, qtile = wk.qtile;
     const int hkv = hq / (int)p.head_q_per_group;
 
     const int Sq = (int)p.seqlen_q, Sk = (int)p.seqlen_kv, D = (int)p.headdim;
@@ -522,6 +561,31 @@ __device__ __forceinline__ void mfma_sv(const bool first, f32x16 &acc, const u32
     }
 }
 
+// Q fragments pinned in AGPRs a[128 + 4*(X*KS + ks)] (fa_agpr_asm.inc): write one, and one MFMA of
+// S^T = K.Q^T reading it as the B operand
+template <int QB>
+__device__ __forceinline__ void agpr_qset(const u32x4 &v) {
+#define FA_CASE(N) \
+    if constexpr (QB == N) fa_agpr_qset_##N(v[0], v[1], v[2], v[3]);
+    FA_CASE(128) FA_CASE(132) FA_CASE(136) FA_CASE(140) FA_CASE(144) FA_CASE(148) FA_CASE(152) FA_CASE(156)
+    FA_CASE(160) FA_CASE(164) FA_CASE(168) FA_CASE(172) FA_CASE(176) FA_CASE(180) FA_CASE(184) FA_CASE(188)
+#undef FA_CASE
+}
+template <bool kF16, int QB>
+__device__ __forceinline__ void mfma_sq(const bool first, f32x16 &acc, const u32x4 &a) {
+#define FA_CASE(N)                                                                         \
+    if constexpr (QB == N) {                                                               \
+        if (first) {                                                                       \
+            if constexpr (kF16) fa_sq_f16_##N##_1(acc, a); else fa_sq_bf16_##N##_1(acc, a); \
+        } else {                                                                           \
+            if constexpr (kF16) fa_sq_f16_##N##_0(acc, a); else fa_sq_bf16_##N##_0(acc, a); \
+        }                                                                                  \
+    }
+    FA_CASE(128) FA_CASE(132) FA_CASE(136) FA_CASE(140) FA_CASE(144) FA_CASE(148) FA_CASE(152) FA_CASE(156)
+    FA_CASE(160) FA_CASE(164) FA_CASE(168) FA_CASE(172) FA_CASE(176) FA_CASE(180) FA_CASE(184) FA_CASE(188)
+#undef FA_CASE
+}
+
 // An asm-issued MFMA's result is invisible to hipcc's hazard recognizer: before the first VALU
 // read of S (or AGPR read of O) after its last MFMA, 21 wait states (32x32x16 = 16 passes).
 __device__ __forceinline__ void s_ready(f32x16 &s0, f32x16 &s1) {
@@ -530,6 +594,8 @@ __device__ __forceinline__ void s_ready(f32x16 &s0, f32x16 &s1) {
 __device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" ::: "memory"); }
 
 #define FA_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+// s_waitcnt lgkmcnt(0) alone (gfx9 encoding: vmcnt 63, expcnt 7, lgkmcnt 0)
+constexpr int kLgkm0 = 0xC07F;
 
 // Opaque redefinition: ties a value to this point of the (volatile-asm ordered) instruction stream,
 // so IR-level sinking / hoisting cannot move the VALU slices out of their MFMA gap.
@@ -541,46 +607,27 @@ __device__ __forceinline__ uint32_t lds_u32(const void *ptr) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)ptr;
 }
 
-// LDS-DMA of NP 1-KiB pieces (one per wave-instruction) from rs + voff[n] to LDS lds0 + n*1024.
+// one LDS-DMA piece (1 KiB per wave-instruction) from rs + voff to LDS address `lds`.
 // Issued from asm so hipcc does not see an LDS write it cannot disambiguate (it would otherwise
 // wait vmcnt(0) before the next ds_read of any slot); the caller retires it with an explicit
-// s_waitcnt vmcnt(0) before the tile's barrier. M0 is saved and restored around the statement.
+// s_waitcnt vmcnt(0) before the tile's barrier. M0 is an asm input ("{m0}"): hipcc materialises it
+// with one s_mov_b32 and keeps its own M0 bookkeeping; the s_nop 0 is the one wait state between
+// an SALU write of M0 and an LDS-DMA that reads it (what hipcc inserts for its own LDS-DMA).
+// nop: 5 more wait states ahead of the descriptor read (a VALU write of those SGPRs is invisible
+// to the hazard recognizer).
+__device__ __forceinline__ void dma_one(const rsrc_t &rs, const uint32_t lds, const int voff, const bool nop) {
+    if (nop)
+        asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "{m0}"(lds)
+                     : "memory");
+    else
+        asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "{m0}"(lds)
+                     : "memory");
+}
+// NP pieces from rs + voff[n] to LDS lds0 + n*1024
 template <int NP>
 __device__ __forceinline__ void dma_pieces(const rsrc_t &rs, const uint32_t lds0, const int *voff) {
-    uint32_t keep;
-    if constexpr (NP == 4)
-        asm volatile(
-            "s_mov_b32 %0, m0\n\ts_nop 4\n\t"
-            "s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %6, 0 offen lds\n\t"
-            "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %3, %6, 0 offen lds\n\t"
-            "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %4, %6, 0 offen lds\n\t"
-            "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %5, %6, 0 offen lds\n\t"
-            "s_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "s"(lds0), "v"(voff[0]), "v"(voff[1]), "v"(voff[2]), "v"(voff[3]), "s"(rs)
-            : "memory", "scc");
-    else
-        asm volatile(
-            "s_mov_b32 %0, m0\n\ts_nop 4\n\t"
-            "s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %4, 0 offen lds\n\t"
-            "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tbuffer_load_dwordx4 %3, %4, 0 offen lds\n\t"
-            "s_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "s"(lds0), "v"(voff[0]), "v"(voff[1]), "s"(rs)
-            : "memory", "scc");
-}
-// one LDS-DMA piece (1 KiB per wave-instruction) from rs + voff to LDS lds; nop: 5 wait states
-// ahead of the descriptor read (a VALU write of those SGPRs is invisible to the hazard recognizer)
-__device__ __forceinline__ void dma_one(const rsrc_t &rs, const uint32_t lds, const int voff, const bool nop) {
-    uint32_t keep;
-    if (nop)
-        asm volatile("s_mov_b32 %0, m0\n\ts_nop 4\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
-                     "buffer_load_dwordx4 %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep) : "s"(lds), "v"(voff), "s"(rs) : "memory");
-    else
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
-                     "buffer_load_dwordx4 %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep) : "s"(lds), "v"(voff), "s"(rs) : "memory");
+#pragma unroll
+    for (int n = 0; n < NP; ++n) dma_one(rs, lds0 + n * 1024, voff[n], n == 0);
 }
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
@@ -603,7 +650,17 @@ __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" :
 // has been drained.
 // =============================================================================================
 template <class DT, bool kCausal, int kD, bool kExactD>
-__global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const int n_qtiles, const int dbg) {
+__global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const int n_qtiles, const int dbg,
+                                                    unsigned long long *stamps) {
+    // Diagnostic build only (-DFA_STAMPS=1, scripts/stamps.py): per-wave s_memtime phase totals.
+#ifdef FA_STAMPS
+    unsigned long long st_t0 = __builtin_amdgcn_s_memtime(), st_rt0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define FA_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+    (void)stamps;
+#define FA_STAMP(v)
+#endif
     using G = Geo<kD>;
     constexpr bool F = DT::kIsF16;
     constexpr int KS = G::kKSteps;
@@ -612,12 +669,11 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     constexpr int T = G::kTileBytes;
     constexpr int NP = T / 4 / 1024;  // LDS-DMA pieces per wave per K or V tile (4 / 2)
     constexpr int ROWS_PER_PIECE = 1024 / RB;
-    constexpr int LA = 32 * DTL, LB = 32 * DTL + 16;  // row-sum accumulators (AGPR bases)
-    // LDS: K slots 0,1 | V slots 0,1 | Q of the 4 waves (64 rows each). K and V sit below 64 KiB
-    // so every fragment read is a per-lane base plus a 16-bit immediate offset.
+    constexpr int QB = 128;  // Q fragments: AGPRs a[QB + 4*(X*KS + ks)] (fa_agpr_asm.inc)
+    // LDS: K slots 0,1 | V slots 0,1 (64 KiB at D = 128), so every fragment read is a per-lane base
+    // plus a 16-bit immediate offset. Q is read once from HBM straight into AGPRs.
     constexpr int KV0 = 0;
-    constexpr int QOFF = 4 * T;
-    __shared__ __attribute__((aligned(1024))) char lds[QOFF + 4 * T];
+    __shared__ __attribute__((aligned(1024))) char lds[4 * T];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -626,15 +682,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     const int h = lane >> 5;
 
     // ---- XCD-aware work decode (as fa_fwd_w8) ------------------------------------------
-    const uint32_t nwg = gridDim.x;
-    const uint32_t bid = blockIdx.x;
-    const uint32_t xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const uint32_t w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-    const uint32_t t = w % (uint32_t)n_qtiles;
-    const uint32_t bh = w / (uint32_t)n_qtiles;
-    const int hq = (int)(bh % (uint32_t)p.num_heads_q);
-    const int b = (int)(bh / (uint32_t)p.num_heads_q);
-    const int qtile = kCausal ? (n_qtiles - 1 - (int)t) : (int)t;
+    const Work wk = decode_work<kCausal>(gridDim.x, blockIdx.x, n_qtiles, (int)p.num_heads_q);
+    const int hq = wk.hq, b = wk.b, qtile = wk.qtile;
     const int hkv = hq / (int)p.head_q_per_group;
 
     const int Sq = (int)p.seqlen_q, Sk = (int)p.seqlen_kv, D = (int)p.headdim;
@@ -667,21 +716,21 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     n_pipe = min(n_pipe, n_end);
     if (dbg & 1) n_pipe = 0;  // debug: every tile through the non-pipelined body
 
-    // ---- Q: this wave's 64 rows go to LDS once (LDS-DMA, K-style swizzle on the source side) --
-    const int qs = (int)p.q_seqlen_stride;
-    char *const Qw = lds + QOFF + wave * T;
+    // ---- Q: this wave's 64 rows, B-operand fragments straight from HBM into AGPRs ----------
+    // lane (h, r) of block X holds Q[mw + 32X + r][16*ks + 8*h + 0..7]; rows >= Sq read as 0
     {
+        const int qs = (int)p.q_seqlen_stride;
         const rsrc_t qr = make_rsrc(qb + 2 * (int64_t)mw * qs, slab_bytes(min(Sq - mw, 64), qs, D));
-        int qoff[4 * NP];
+        u32x4 qv[2 * KS];
 #pragma unroll
-        for (int n = 0; n < 4 * NP; ++n) {
-            const int row = n * ROWS_PER_PIECE + (16 * lane) / RB;
-            const int slot = ((16 * lane) % RB) / 16;
-            const int ch = G::k_off(row, slot) % RB / 16;
-            qoff[n] = (kExactD || ch * 8 < D) ? row * qs * 2 + 16 * ch : 0x7ffffff0;  // past the end -> 0
-        }
+        for (int X = 0; X < 2; ++X)
 #pragma unroll
-        for (int n = 0; n < 4; ++n) dma_pieces<NP>(qr, lds_u32(Qw) + n * NP * 1024, qoff + n * NP);
+            for (int ks = 0; ks < KS; ++ks) {
+                const bool ok = kExactD || 16 * ks + 8 * h < D;  // columns past D read as 0
+                qv[X * KS + ks] = __builtin_amdgcn_raw_buffer_load_b128(
+                    qr, ok ? (32 * X + r) * qs * 2 + 32 * ks + 16 * h : 0x7ffffff0, 0, 0);
+            }
+        static_for<2 * KS>([&](auto I) { agpr_qset<QB + 4 * decltype(I)::value>(qv[decltype(I)::value]); });
     }
 
     // ---- LDS-DMA staging: this wave writes pieces (wave*NP + n) of each K and V tile --------
@@ -718,12 +767,6 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     int k_addr[KS];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) k_addr[ks] = G::k_off(r, 2 * ks + h);
-    // Q fragment addresses (above 64 KiB, so absolute per k-step; block B is +32 rows)
-    int q_addr[KS];
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) q_addr[ks] = (int)lds_u32(Qw) + k_addr[ks];
-    typedef __attribute__((address_space(3))) const u32x4 lds_u32x4;
-    auto qread = [&](int ks, int boff) { return *(lds_u32x4 *)(uintptr_t)(q_addr[ks] + boff); };
     // ---- state ------------------------------------------------------------------------------
     struct Sm {               // online-softmax state of one block (per lane: one query row)
         float m, msc, alpha;  // running max (unscaled), m*sc, alpha of the last decision
@@ -794,7 +837,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     };
 
     // ---- phase 1: S[c] = K.Q^T for both blocks (4*KS single MFMAs) ----------------------------
-    // gap g (after MFMA g): next k-step's K / Q fragments (gaps 4ks, 4ks+1), one LDS-DMA piece
+    // gap g (after MFMA g): next k-step's K fragments (gaps 4ks, 4ks+1; Q is in AGPRs), one LDS-DMA piece
     // (gap 4ks+2: K_{j+1} pieces, then V_j pieces), and with SM2 the second softmax half of the
     // tile of parity pr (32 units: block u&1, score u>>1 of half 1).
     constexpr int G1 = 4 * KS;
@@ -802,19 +845,18 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                       const uint32_t k_lds, const uint32_t v_lds) {
         constexpr int c = decltype(PAR)::value, pr = c ^ 1;
         constexpr bool do_sm = decltype(SM2)::value, do_dma = decltype(DMA)::value;
-        u32x4 kf[2][2], qf[2][2];  // [buffer][key half | block]
+        u32x4 kf[2][2];  // [buffer][key half]
 #pragma unroll
-        for (int x = 0; x < 2; ++x) {
-            kf[0][x] = *(const u32x4 *)(K + x * 32 * RB + k_addr[0]);
-            qf[0][x] = qread(0, x * 32 * RB);
-        }
+        for (int x = 0; x < 2; ++x) kf[0][x] = *(const u32x4 *)(K + x * 32 * RB + k_addr[0]);
         static_for<G1>([&](auto G) {
             constexpr int g = decltype(G)::value;
             constexpr int ks = g >> 2, i = g & 3, cb = ks & 1;
-            mfma_sv<F>(ks == 0, S[c][i], kf[cb][i & 1], qf[cb][i >> 1]);
-            if constexpr (ks + 1 < KS && i < 2) {
-                kf[cb ^ 1][i] = *(const u32x4 *)(K + i * 32 * RB + k_addr[ks + 1]);
-                qf[cb ^ 1][i] = qread(ks + 1, i * 32 * RB);
+            // one counted wait per k-step (its two K fragments were read a whole k-step ahead)
+            if constexpr (ks > 0 && i == 0) __builtin_amdgcn_s_waitcnt(kLgkm0);
+            mfma_sq<F, QB + 4 * ((i >> 1) * KS + ks)>(ks == 0, S[c][i], kf[cb][i & 1]);
+            if constexpr (ks + 1 < KS && i == 0) {
+                kf[cb ^ 1][0] = *(const u32x4 *)(K + k_addr[ks + 1]);
+                kf[cb ^ 1][1] = *(const u32x4 *)(K + 32 * RB + k_addr[ks + 1]);
             }
             if constexpr (do_dma && i == 2) {
                 if constexpr (ks < NP) dma_one(kr, k_lds + ks * 1024, kvo[ks], ks == 0);
@@ -889,8 +931,14 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         static_for<G2>([&](auto G) {
             constexpr int g = decltype(G)::value;
             constexpr int kk = g / (2 * DTL), i = g % (2 * DTL), X = i / DTL, dt = i % DTL;
+            // one counted wait per 16-key step: its V^T fragments were read in the first DTL gaps
+            // of the previous step, two per gap
+            if constexpr (kk > 0 && i == 0) __builtin_amdgcn_s_waitcnt(kLgkm0);
             agpr_mfma<F, X * 16 * DTL + 16 * dt>(va[kk & 1][dt], P[cp][4 * X + kk]);
-            if constexpr (kk + 1 < 4) rd(kk + 1, i, va[(kk + 1) & 1]);
+            if constexpr (kk + 1 < 4 && i < DTL) {
+                rd(kk + 1, 2 * i, va[(kk + 1) & 1]);
+                rd(kk + 1, 2 * i + 1, va[(kk + 1) & 1]);
+            }
             if constexpr (do_sm) {
                 static_for<32>([&](auto M) {
                     constexpr int X2 = decltype(M)::value >> 4, m = decltype(M)::value & 15;
@@ -938,6 +986,16 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         const int key0 = j * kBlockN;
         return make_rsrc(vb + 2 * (int64_t)key0 * vs_, slab_bytes(min(Sk - key0, kBlockN), vs_, D));
     };
+    // pipelined loop: running tile pointers (no 64-bit multiply per tile); a full tile spans
+    // full_k / full_v bytes, the Sk tail tile fewer, a tile past Sk none
+    const uint32_t full_k = slab_bytes(kBlockN, ks_, D), full_v = slab_bytes(kBlockN, vs_, D);
+    const int64_t step_k = 2 * (int64_t)kBlockN * ks_, step_v = 2 * (int64_t)kBlockN * vs_;
+    const char *kp = kb + step_k;  // K tile j + 1 of iteration j
+    const char *vp = vb;           // V tile j of iteration j
+    auto tile_bytes = [&](const int key0, const uint32_t full, const int stride) {
+        const int rows = Sk - key0;
+        return rows >= kBlockN ? full : slab_bytes(rows, stride, D);
+    };
     const uint32_t lds_base = lds_u32(lds) + wave * NP * 1024;  // this wave's pieces of slot 0
 
     // ---- prologue -------------------------------------------------------------------------
@@ -956,19 +1014,34 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         for (int i = 0; i < per_thread; ++i) *(u32x4 *)(lds + KV0 + 3 * T + (i * 256 + tid) * 16) = (u32x4){0, 0, 0, 0};
     }
     if (n_end > 0) stage_k(0);
-    dma_wait();       // Q and K_0 landed
+    dma_wait();       // K_0 landed
     __syncthreads();  // visible to every wave
 
     // ---- pipelined tiles: iteration j = P1(S_j || softmax half 2 of j-1, DMA K_{j+1}, V_j),
     //      P2(O += P_{j-1} V_{j-1} || softmax half 1 of j), rescale, barrier -------------------
     auto iter = [&](const int j, auto PAR) {
         constexpr int c = decltype(PAR)::value, pr = c ^ 1;
-        const rsrc_t kr = k_rsrc(j + 1), vr = v_rsrc(j);
+        FA_STAMP(sa);
+        const rsrc_t kr = make_rsrc(kp, tile_bytes((j + 1) * kBlockN, full_k, ks_));
+        const rsrc_t vr = make_rsrc(vp, tile_bytes(j * kBlockN, full_v, vs_));
+        kp += step_k;
+        vp += step_v;
         phase1(lds + KV0 + c * T, PAR, IC<1>{}, IC<1>{}, kr, vr, lds_base + pr * T, lds_base + (2 + c) * T);
+        FA_STAMP(sb);
         phase2(lds + KV0 + (2 + pr) * T, IC<pr>{}, PAR, IC<1>{});
         rescale();
+        FA_STAMP(sc_);
         dma_wait();  // K_{j+1}, V_j landed
+        FA_STAMP(sd);
         __syncthreads();
+#ifdef FA_STAMPS
+        const unsigned long long se = __builtin_amdgcn_s_memtime();
+        st_acc[0] += sb - sa;
+        st_acc[1] += sc_ - sb;
+        st_acc[2] += sd - sc_;
+        st_acc[3] += se - sd;
+        st_acc[4] += 1;
+#endif
     };
     for (int j = 0; j < n_pipe; j += 2) {
         iter(j, IC<0>{});
@@ -984,6 +1057,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         if ((n_pipe - 1) & 1) drain(IC<1>{}); else drain(IC<0>{});
     }
 
+    FA_STAMP(s_pipe_end);
     // ---- remaining tiles: masked, not pipelined --------------------------------------------
     if (n_pipe < n_end) {
         stage_v(n_pipe);  // the pipeline fetched V one tile late; catch up before the first one
@@ -1053,9 +1127,28 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             }
         }
     };
+    FA_STAMP(s_masked_end);
     store_block(r, IC<0>{}, st[0].l);
     store_block(r + 32, IC<16 * DTL>{}, st[1].l);
+#ifdef FA_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+    const unsigned long long s_end = __builtin_amdgcn_s_memtime(), rt_end = __builtin_amdgcn_s_memrealtime();
+    if (stamps && lane == 0) {
+        // [total, p1, p2+rescale, dma wait, barrier, tiles, pipelined-loop span, masked tiles,
+        //  epilogue, realtime (100 MHz ticks), start time]
+        unsigned long long *o = stamps + ((size_t)blockIdx.x * 4 + wave) * 12;
+        o[0] = s_end - st_t0;
+        for (int i = 0; i < 5; ++i) o[1 + i] = st_acc[i];
+        o[6] = s_pipe_end - st_t0;
+        o[7] = s_masked_end - s_pipe_end;
+        o[8] = s_end - s_masked_end;
+        o[9] = rt_end - st_rt0;
+        o[10] = st_t0;
+        o[11] = xcc_id();
+    }
+#endif
 }
+#undef FA_STAMP
 
 // ---- host launch of one instantiation -------------------------------------------------
 template <class DT, bool C, int kD, bool kExact>
@@ -1068,7 +1161,7 @@ int launch_one(const fa_fwd_params &p, hipStream_t stream) {
                            (int)n_qtiles);
     else
         hipLaunchKernelGGL((fa_fwd_w4<DT, C, kD, kExact>), dim3((uint32_t)nwg), dim3(256), 0, stream, p,
-                           (int)n_qtiles, variant == 2 ? 1 : 0);
+                           (int)n_qtiles, variant == 2 ? 1 : 0, stamp_buffer());
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "HIP launch failed: %s", hipGetErrorString(e));
     return FA_OK;

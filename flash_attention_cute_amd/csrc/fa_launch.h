@@ -32,6 +32,10 @@ inline int variant_from_env() {
     return 0;
 }
 
+// diagnostic per-wave phase stamps of fa_fwd_w4 (only a -DFA_STAMPS=1 build writes them; see
+// fa_debug_set_stamps in fa_fwd_gfx950.hip and scripts/stamps.py); nullptr otherwise
+unsigned long long *stamp_buffer();
+
 // launch one (dtype, causal, head-dim tile, exact head dim) instantiation on `stream`
 template <class DT, bool C, int kD, bool kExact>
 int launch_one(const fa_fwd_params &p, hipStream_t stream);

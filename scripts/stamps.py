@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""In-kernel phase stamps of fa_fwd_w4 (diagnostic; needs the -DFA_STAMPS=1 build:
+python -c "from flash_attention_cute_amd import _build; _build.build_abi(stamps=True)").
+
+Loads build/stamps/libfa_gfx950.so through its C-ABI, runs ~2 s of back-to-back launches of one
+bench config (DVFS settles), then one stamped launch, and prints per-wave medians of the cycle
+split: phase 1 (S = K.Q^T || softmax 2 || DMA), phase 2 (O += P.V || softmax 1) + rescale, the
+DMA wait, the barrier; plus the in-kernel clock (s_memtime / s_memrealtime x 100 MHz).
+usage: python scripts/stamps.py [c2|c3|c4|c5]
+"""
+import ctypes
+import sys
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+import bench  # noqa: E402
+
+cfg = bench.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "c2"]
+lib = ctypes.CDLL(str(ROOT / "build" / "stamps" / "libfa_gfx950.so"))
+
+
+class P(ctypes.Structure):
+    _fields_ = ([(n, ctypes.c_void_p) for n in ("q", "k", "v", "o")]
+                + [(n, ctypes.c_int64) for n in ("B", "Hq", "Hkv", "Sq", "Sk", "D", "g")]
+                + [(f"s{i}", ctypes.c_int64) for i in range(12)] + [("scale", ctypes.c_float)])
+
+
+dev = torch.device("cuda:0")
+dt = torch.float16 if cfg["dtype"] == "fp16" else torch.bfloat16
+torch.manual_seed(0)
+q = torch.randn(cfg["B"], cfg["Hq"], cfg["Sq"], cfg["D"], device=dev, dtype=dt)
+k = torch.randn(cfg["B"], cfg["Hkv"], cfg["Sk"], cfg["D"], device=dev, dtype=dt)
+v = torch.randn_like(k)
+o = torch.empty_like(q)
+st = []
+for t in (q, k, v, o):
+    st.append(t)
+p = P(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), cfg["B"], cfg["Hq"], cfg["Hkv"], cfg["Sq"],
+      cfg["Sk"], cfg["D"], cfg["Hq"] // cfg["Hkv"],
+      *[t.stride(0) for t in st], *[t.stride(1) for t in st], *[t.stride(2) for t in st],
+      cfg["D"] ** -0.5 * 1.4426950408889634)
+nwg = cfg["B"] * cfg["Hq"] * ((cfg["Sq"] + 255) // 256)
+buf = torch.zeros(nwg * 4 * 12, dtype=torch.int64, device=dev)
+stream = torch.cuda.current_stream().cuda_stream
+lib.fa_debug_set_stamps(ctypes.c_void_p(0))
+import time  # noqa: E402
+
+t0 = time.time()
+n = 0
+while time.time() - t0 < 2.0:
+    assert lib.fa_fwd_gfx950(ctypes.byref(p), 0 if dt == torch.float16 else 1, int(cfg["causal"]),
+                             ctypes.c_void_p(stream)) == 0
+    n += 1
+    if n % 20 == 0:
+        torch.cuda.synchronize()
+lib.fa_debug_set_stamps(ctypes.c_void_p(buf.data_ptr()))
+assert lib.fa_fwd_gfx950(ctypes.byref(p), 0 if dt == torch.float16 else 1, int(cfg["causal"]),
+                         ctypes.c_void_p(stream)) == 0
+torch.cuda.synchronize()
+lib.fa_debug_set_stamps(ctypes.c_void_p(0))
+s = buf.view(-1, 12).cpu().double()
+names = ["total", "p1", "p2+resc", "dma_wait", "barrier", "tiles", "pipe_span", "masked", "epilogue", "realtime"]
+med = s.median(dim=0).values
+print(f"{cfg['workload']}: {n} warm launches, {s.shape[0]} waves")
+for i, nm in enumerate(names):
+    print(f"  {nm:10s} median {med[i]:12.0f}  mean {s[:, i].mean():12.0f}")
+tiles = s[:, 5].clamp(min=1)
+for i, nm in [(1, "p1"), (2, "p2+resc"), (3, "dma_wait"), (4, "barrier")]:
+    print(f"  per tile {nm:10s} {float((s[:, i] / tiles).median()):8.0f} cycles")
+clk = (s[:, 0] / s[:, 9] * 100e6 / 1e9)
+print(f"  in-kernel clock median {float(clk.median()):.3f} GHz")
+start = s[:, 10] - s[:, 10].min()
+print(f"  launch span {float((s[:, 10] + s[:, 0]).max() - s[:, 10].min()):.0f} cycles, start spread "
+      f"{float(start.max()):.0f}")
