@@ -1,0 +1,371 @@
+#pragma once
+// fa_decode.hpp -- split-KV ("flash-decoding") forward for few query rows per kv-head, gfx950.
+//
+// The reference has no split-KV kernel (TODO at reference README.md:20). Its decode path is the
+// q-head pack of reference csrc/flash_attention_api.cpp:72-83: with Sq == 1 the group of q-heads
+// that share one kv-head becomes the rows of one problem, and the prefill kernel then runs one
+// 128-row CTA per (batch, kv-head) over the whole K/V stream -- B * Hkv CTAs, most rows empty.
+// Decode is HBM-bound (every K/V byte is read once per step), so this kernel is built around the
+// K/V stream instead of the MFMA:
+//
+//   * a row block is up to 32 (q-head, position) rows of one (batch, kv-head): rows_total =
+//     head_q_per_group * Sq, row r -> q-head hkv * g + r / Sq, position r % Sq. The host's Sq == 1
+//     pack (g' = 1, Sq' = g) and unpacked GQA with a few query positions (speculative decode,
+//     causal per position) map onto the same rows; K/V are read once per group either way;
+//   * one workgroup = 4 wave64s on one (batch, kv-head, row block, key split); each wave owns a
+//     contiguous quarter of the split's 32-key tiles and streams them through its OWN 2-slot
+//     LDS ring by LDS-DMA (buffer_load ... lds, 1 KiB per wave-instruction, XOR swizzle applied
+//     on the source offsets as in fa_fwd_w4). No barrier in the key loop: a wave only waits for
+//     its own DMA (vmcnt);
+//   * per tile S^T = K.Q^T and O^T += V^T.P^T with v_mfma_f32_32x32x16 (fragment layouts of
+//     fa_fwd_w8: each lane owns one row, the rounded P^T is directly the B operand); MFMA time is
+//     ~1/4 of the tile's HBM time at 1 wave per SIMD, so padding rows to 32 costs nothing;
+//   * the 4 wave partials are merged in LDS (log-sum-exp weights); with n_split == 1 the
+//     workgroup writes O, otherwise fp32 partials (O / l and lse) go to a caller-provided
+//     workspace and fa_decode_combine merges the splits.
+//
+// Numerics: S in fp32, P = exp2(S*s' - m*s') rounded (RNE) to T before P.V, row sums of the fp32
+// P, deferred max (guide T13, as fa_fwd_w4). The split changes only which running max a P is
+// rounded against, which is within the stated fp16 / bf16 tolerance (tests/test_gpu_parity.py).
+// Rows that see no key are 0 (DESIGN.md quirk iii).
+#include "fa_fwd_kernels.hpp"
+
+namespace fa {
+
+template <int kD>
+struct DecGeo {
+    using G = Geo<kD>;
+    static constexpr int RB = G::kRowBytes;
+    static constexpr int kTile = kDecKeys * RB;     // bytes of one K (or V) tile: 8 / 4 KiB
+    static constexpr int kPieces = kTile / 1024;    // LDS-DMA pieces per K (or V) tile
+    static constexpr int kSlot = 2 * kTile;         // K + V
+    static constexpr int kWaveLds = 2 * kSlot;      // 2-slot ring per wave
+    static constexpr int kLds = kDecWaves * kWaveLds;
+    static constexpr int kQPiecesPerWave = kDecRows * RB / 1024 / kDecWaves;  // 2 / 1
+};
+
+template <class DT, bool kCausal, int kD, bool kExactD>
+__global__ __launch_bounds__(256, 1) void fa_decode(const fa_fwd_params p, const DecArgs a) {
+    using G = Geo<kD>;
+    using DG = DecGeo<kD>;
+    constexpr int KS = G::kKSteps;
+    constexpr int DTL = G::kDTiles;
+    constexpr int RB = DG::RB;
+    constexpr int NP = DG::kPieces;
+    __shared__ __attribute__((aligned(1024))) char lds[DG::kLds];
+    __shared__ __attribute__((aligned(1024))) char qlds[kDecRows * RB];
+    __shared__ float ml[kDecWaves][kDecRows][2];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31;
+    const int h = lane >> 5;
+
+    // ---- work: (unit = (b, hkv, rb), split) ----------------------------------------------------
+    const int split = blockIdx.x % a.n_split;
+    const int unit = blockIdx.x / a.n_split;
+    const int rb = unit % a.n_rb;
+    const int hkv = (unit / a.n_rb) % (int)p.num_heads_kv;
+    const int b = unit / (a.n_rb * (int)p.num_heads_kv);
+    const int Sq = (int)p.seqlen_q, Sk = (int)p.seqlen_kv, D = (int)p.headdim;
+    const float sc = p.softmax_scale;
+    const float thr_raw = kRescaleThr / sc;
+    const int diag = Sk - Sq;
+
+    // this lane's row
+    const int rg = rb * kDecRows + r;
+    const bool row_ok = rg < a.rows;
+    const int pos = row_ok ? rg % Sq : 0;
+    const int lim = (kCausal && row_ok) ? min(Sk - 1, pos + diag) : Sk - 1;  // last visible key
+
+    // ---- this wave's tiles: a contiguous quarter of the split --------------------------------
+    const int n_tiles = (Sk + kDecKeys - 1) / kDecKeys;
+    const int s_lo = min(split * a.tps, n_tiles), s_hi = min(s_lo + a.tps, n_tiles);
+    const int per_wave = (s_hi - s_lo + kDecWaves - 1) / kDecWaves;
+    const int t_lo = min(s_lo + wave * per_wave, s_hi), t_hi = min(t_lo + per_wave, s_hi);
+
+    const char *kb = (const char *)p.k_ptr + 2 * ((int64_t)b * p.k_batch_stride + (int64_t)hkv * p.k_head_stride);
+    const char *vb = (const char *)p.v_ptr + 2 * ((int64_t)b * p.v_batch_stride + (int64_t)hkv * p.v_head_stride);
+    const int ks_ = (int)p.k_seqlen_stride, vs_ = (int)p.v_seqlen_stride;
+
+    // ---- LDS-DMA source offsets (lane-linear destination, swizzle on the source) ---------------
+    constexpr int ROWS_PER_PIECE = 1024 / RB;
+    int kvo[NP], vvo[NP];
+#pragma unroll
+    for (int n = 0; n < NP; ++n) {
+        const int row = n * ROWS_PER_PIECE + (16 * lane) / RB;
+        const int slot = ((16 * lane) % RB) / 16;
+        const int kch = G::k_off(row, slot) % RB / 16;
+        const int vch = G::v_off(row, slot) % RB / 16;
+        kvo[n] = (kExactD || kch * 8 < D) ? row * ks_ * 2 + 16 * kch : 0x7ffffff0;
+        vvo[n] = (kExactD || vch * 8 < D) ? row * vs_ * 2 + 16 * vch : 0x7ffffff0;
+    }
+    char *ring = lds + wave * DG::kWaveLds;
+    const uint32_t ring_u = lds_u32(ring);
+    auto issue = [&](const int t) {
+        const int key0 = t * kDecKeys;
+        const int rows = min(Sk - key0, kDecKeys);
+        const uint32_t dst = ring_u + (t & 1) * DG::kSlot;
+        const rsrc_t kr = make_rsrc(kb + 2 * (int64_t)key0 * ks_, slab_bytes(rows, ks_, D));
+        const rsrc_t vr = make_rsrc(vb + 2 * (int64_t)key0 * vs_, slab_bytes(rows, vs_, D));
+#pragma unroll
+        for (int n = 0; n < NP; ++n) dma_one(kr, dst + n * 1024, kvo[n], n == 0);
+#pragma unroll
+        for (int n = 0; n < NP; ++n) dma_one(vr, dst + DG::kTile + n * 1024, vvo[n], n == 0);
+    };
+    // ---- Q: the row block's 32 rows by LDS-DMA into a shared K-swizzled image -----------------
+    // (rows are scattered over q-heads / positions; a descriptor over the group's span bounds
+    // them, invalid rows and columns past D read 0). Issued before the K/V tiles so that the
+    // counted wait below retires it.
+    {
+        const int64_t qspan = ((int64_t)(a.g - 1) * p.q_head_stride + (int64_t)(Sq - 1) * p.q_seqlen_stride + D) * 2;
+        const rsrc_t qr = make_rsrc((const char *)p.q_ptr + 2 * ((int64_t)b * p.q_batch_stride +
+                                                                 (int64_t)hkv * a.g * p.q_head_stride),
+                                    (uint32_t)qspan);
+#pragma unroll
+        for (int n = 0; n < DG::kQPiecesPerWave; ++n) {
+            const int piece = wave * DG::kQPiecesPerWave + n;
+            const int row = piece * ROWS_PER_PIECE + (16 * lane) / RB;
+            const int slot = ((16 * lane) % RB) / 16;
+            const int ch = G::k_off(row, slot) % RB / 16;
+            const int rq = rb * kDecRows + row;
+            const int off = (rq < a.rows && (kExactD || ch * 8 < D))
+                                ? 2 * ((rq / Sq) * (int)p.q_head_stride + (rq % Sq) * (int)p.q_seqlen_stride) + 16 * ch
+                                : 0x7ffffff0;
+            dma_one(qr, lds_u32(qlds) + piece * 1024, off, n == 0);
+        }
+    }
+    const bool has0 = t_lo < t_hi, has1 = t_lo + 1 < t_hi;
+    if (has0) issue(t_lo);
+    if (has1) issue(t_lo + 1);
+    if (has1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * NP) : "memory");
+    else if (has0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NP) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave's Q pieces landed
+    // B operand of S^T = K.Q^T: lane (h, r) holds Q[row r][16 ks + 8 h .. +7]
+    u32x4 qf[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = *(const u32x4 *)(qlds + G::k_off(r, 2 * ks + h));
+
+    // ---- per-lane LDS fragment addresses (fa_fwd_w8 layouts) ----------------------------------
+    const int g4 = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+    int v_addr[DTL];
+#pragma unroll
+    for (int dt = 0; dt < DTL; ++dt)
+        v_addr[dt] = G::v_off(4 * (g4 >> 1) + qq, dt * 4 + 2 * (g4 & 1) + (pp >> 1)) + 8 * (pp & 1);
+    int k_addr[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) k_addr[ks] = G::k_off(r, 2 * ks + h);
+
+    f32x16 o[DTL];
+#pragma unroll
+    for (int dt = 0; dt < DTL; ++dt) o[dt] = (f32x16){};
+    float m_use = kNeg, msc = 0.f, l_run = 0.f;
+
+    for (int t = t_lo; t < t_hi; ++t) {
+        // tile t landed (the youngest 2*NP pieces, tile t+1, may still be in flight)
+        if (t + 1 < t_hi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NP) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const char *K = ring + (t & 1) * DG::kSlot;
+        const char *V = K + DG::kTile;
+        u32x4 kf[KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) kf[ks] = *(const u32x4 *)(K + k_addr[ks]);
+        u32x4 va[2][DTL];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int dt = 0; dt < DTL; ++dt) {
+                const u32x2 lo = tr_read(V + kk * 16 * RB + v_addr[dt]);
+                const u32x2 hi = tr_read(V + kk * 16 * RB + 8 * RB + v_addr[dt]);
+                va[kk][dt] = (u32x4){lo[0], lo[1], hi[0], hi[1]};
+            }
+        // the slot is free once its fragments are in registers: refill it with tile t+2
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (t + 2 < t_hi) issue(t + 2);
+
+        f32x16 s = {};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) s = DT::mfma(kf[ks], qf[ks], s);
+
+        const int key0 = t * kDecKeys;
+        // lane (h, r) holds keys key0 + (i & 3) + 8 (i >> 2) + 4 h of row r
+        if (__builtin_amdgcn_ballot_w64(key0 + kDecKeys - 1 > lim)) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                if (key0 + (i & 3) + 8 * (i >> 2) + 4 * h > lim) s[i] = kNeg;
+        }
+        float mx = fmaxf(s[0], s[1]);
+#pragma unroll
+        for (int i = 2; i < 16; ++i) mx = fmaxf(mx, s[i]);
+        mx = pair_max(mx);
+        if (__builtin_amdgcn_ballot_w64(mx > m_use + thr_raw)) {
+            const float m_new = fmaxf(m_use, mx);
+            const float msc_new = (m_new <= 0.5f * kNeg) ? 0.f : m_new * sc;
+            // a row's first visible key: O and l are still 0, alpha must not overflow
+            const float alpha = (m_use <= 0.5f * kNeg) ? 0.f : __builtin_amdgcn_exp2f(msc - msc_new);
+            m_use = m_new;
+            msc = msc_new;
+            l_run *= alpha;
+#pragma unroll
+            for (int dt = 0; dt < DTL; ++dt) o[dt] *= alpha;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[i], sc, -msc));
+        float ls = s[0];
+#pragma unroll
+        for (int i = 1; i < 16; ++i) ls += s[i];
+        l_run += ls;
+        u32x4 pf[2];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+            pf[kk] = (u32x4){DT::pack(s[8 * kk + 0], s[8 * kk + 1]), DT::pack(s[8 * kk + 2], s[8 * kk + 3]),
+                             DT::pack(s[8 * kk + 4], s[8 * kk + 5]), DT::pack(s[8 * kk + 6], s[8 * kk + 7])};
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int dt = 0; dt < DTL; ++dt) o[dt] = DT::mfma(va[kk][dt], pf[kk], o[dt]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    // ---- merge the 4 wave partials in LDS ------------------------------------------------------
+    __syncthreads();  // every wave is done with its ring
+    float *ow = (float *)lds;  // [wave][row][kD]
+    {
+        const float l_tot = pair_sum(l_run);
+        if (h == 0) {
+            ml[wave][r][0] = (m_use <= 0.5f * kNeg) ? kNeg : msc;
+            ml[wave][r][1] = l_tot;
+        }
+#pragma unroll
+        for (int dt = 0; dt < DTL; ++dt)
+#pragma unroll
+            for (int grp = 0; grp < 4; ++grp) {
+                const int d = dt * 32 + 8 * grp + 4 * h;
+                *(float4 *)(ow + (wave * kDecRows + r) * kD + d) =
+                    make_float4(o[dt][4 * grp], o[dt][4 * grp + 1], o[dt][4 * grp + 2], o[dt][4 * grp + 3]);
+            }
+    }
+    __syncthreads();
+
+    constexpr int DPT = kD / 8;  // d values per thread: thread (row = tid / 8, part = tid % 8)
+    const int row = tid >> 3, part = tid & 7;
+    float M = kNeg;
+#pragma unroll
+    for (int w = 0; w < kDecWaves; ++w) M = fmaxf(M, ml[w][row][0]);
+    float wgt[kDecWaves], L = 0.f;
+#pragma unroll
+    for (int w = 0; w < kDecWaves; ++w) {
+        const float mw = ml[w][row][0];
+        wgt[w] = (mw <= 0.5f * kNeg) ? 0.f : __builtin_amdgcn_exp2f(mw - M);
+        L += wgt[w] * ml[w][row][1];
+    }
+    float acc[DPT];
+#pragma unroll
+    for (int i = 0; i < DPT; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int w = 0; w < kDecWaves; ++w) {
+        const float *src = ow + (w * kDecRows + row) * kD + part * DPT;
+#pragma unroll
+        for (int i = 0; i < DPT; i += 4) {
+            const float4 x = *(const float4 *)(src + i);
+            acc[i] += wgt[w] * x.x;
+            acc[i + 1] += wgt[w] * x.y;
+            acc[i + 2] += wgt[w] * x.z;
+            acc[i + 3] += wgt[w] * x.w;
+        }
+    }
+    const float inv = L > 0.f ? 1.f / L : 0.f;
+    const int rg2 = rb * kDecRows + row;
+    if (a.n_split == 1) {
+        if (rg2 < a.rows) {
+            const int hq2 = hkv * a.g + rg2 / Sq, pos2 = rg2 % Sq;
+            char *orow = (char *)p.o_ptr + 2 * ((int64_t)b * p.o_batch_stride + (int64_t)hq2 * p.o_head_stride +
+                                                (int64_t)pos2 * p.o_seqlen_stride);
+#pragma unroll
+            for (int i = 0; i < DPT; i += 8) {
+                const int d = part * DPT + i;
+                if (kExactD || d < D) {
+                    const u32x4 w4 = {DT::pack(acc[i] * inv, acc[i + 1] * inv), DT::pack(acc[i + 2] * inv, acc[i + 3] * inv),
+                                      DT::pack(acc[i + 4] * inv, acc[i + 5] * inv),
+                                      DT::pack(acc[i + 6] * inv, acc[i + 7] * inv)};
+                    *(u32x4 *)(orow + 2 * d) = w4;
+                }
+            }
+        }
+    } else {
+        const size_t slot = (size_t)blockIdx.x * kDecRows + row;  // (unit * n_split + split) * 32 + row
+        float *dst = a.ws_o + slot * kD + part * DPT;
+#pragma unroll
+        for (int i = 0; i < DPT; i += 4)
+            *(float4 *)(dst + i) = make_float4(acc[i] * inv, acc[i + 1] * inv, acc[i + 2] * inv, acc[i + 3] * inv);
+        if (part == 0) a.ws_lse[slot] = L > 0.f ? M + __builtin_amdgcn_logf(L) : kNeg;  // log2
+    }
+}
+
+// Merge n_split partials (O / l and lse = m*s' + log2 l, log2 units) of one row block.
+template <class DT, int kD, bool kExactD>
+__global__ __launch_bounds__(256) void fa_decode_combine(const fa_fwd_params p, const DecArgs a) {
+    constexpr int DPT = kD / 8;
+    const int unit = blockIdx.x;
+    const int rb = unit % a.n_rb;
+    const int hkv = (unit / a.n_rb) % (int)p.num_heads_kv;
+    const int b = unit / (a.n_rb * (int)p.num_heads_kv);
+    const int Sq = (int)p.seqlen_q, D = (int)p.headdim;
+    const int row = threadIdx.x >> 3, part = threadIdx.x & 7;
+    const int rg = rb * kDecRows + row;
+    if (rg >= a.rows) return;
+    const size_t base = (size_t)unit * a.n_split * kDecRows + row;
+    float M = kNeg;
+    for (int s = 0; s < a.n_split; ++s) M = fmaxf(M, a.ws_lse[base + (size_t)s * kDecRows]);
+    float acc[DPT], L = 0.f;
+#pragma unroll
+    for (int i = 0; i < DPT; ++i) acc[i] = 0.f;
+    for (int s = 0; s < a.n_split; ++s) {
+        const size_t slot = base + (size_t)s * kDecRows;
+        const float ls = a.ws_lse[slot];
+        const float w = (ls <= 0.5f * kNeg) ? 0.f : __builtin_amdgcn_exp2f(ls - M);
+        L += w;
+        const float *src = a.ws_o + slot * kD + part * DPT;
+#pragma unroll
+        for (int i = 0; i < DPT; i += 4) {
+            const float4 x = *(const float4 *)(src + i);
+            acc[i] += w * x.x;
+            acc[i + 1] += w * x.y;
+            acc[i + 2] += w * x.z;
+            acc[i + 3] += w * x.w;
+        }
+    }
+    const float inv = L > 0.f ? 1.f / L : 0.f;
+    const int hq = hkv * a.g + rg / Sq, pos = rg % Sq;
+    char *orow = (char *)p.o_ptr +
+                 2 * ((int64_t)b * p.o_batch_stride + (int64_t)hq * p.o_head_stride + (int64_t)pos * p.o_seqlen_stride);
+#pragma unroll
+    for (int i = 0; i < DPT; i += 8) {
+        const int d = part * DPT + i;
+        if (kExactD || d < D) {
+            const u32x4 w4 = {DT::pack(acc[i] * inv, acc[i + 1] * inv), DT::pack(acc[i + 2] * inv, acc[i + 3] * inv),
+                              DT::pack(acc[i + 4] * inv, acc[i + 5] * inv), DT::pack(acc[i + 6] * inv, acc[i + 7] * inv)};
+            *(u32x4 *)(orow + 2 * d) = w4;
+        }
+    }
+}
+
+template <class DT, bool C, int kD, bool kExact>
+int launch_decode(const fa_fwd_params &p, DecArgs a, void *ws, hipStream_t stream) {
+    const int64_t units = decode_units(p, a);
+    if (a.n_split > 1) {
+        const int64_t slots = units * a.n_split * kDecRows;
+        a.ws_o = (float *)ws;
+        a.ws_lse = (float *)((char *)ws + slots * kD * 4);
+    }
+    hipLaunchKernelGGL((fa_decode<DT, C, kD, kExact>), dim3((uint32_t)(units * a.n_split)), dim3(256), 0, stream, p, a);
+    if (a.n_split > 1)
+        hipLaunchKernelGGL((fa_decode_combine<DT, kD, kExact>), dim3((uint32_t)units), dim3(256), 0, stream, p, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "HIP launch failed: %s", hipGetErrorString(e));
+    return FA_OK;
+}
+
+}  // namespace fa

@@ -9,6 +9,7 @@
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "fa_gfx950.h"
@@ -91,6 +92,47 @@ int launch(const fa_fwd_params &p, hipStream_t stream) {
         return p.headdim == 64 ? launch_one<DT, C, 64, true>(p, stream) : launch_one<DT, C, 64, false>(p, stream);
     return p.headdim == 128 ? launch_one<DT, C, 128, true>(p, stream) : launch_one<DT, C, 128, false>(p, stream);
 }
+template <class DT, bool C>
+int launch_dec(const fa_fwd_params &p, const fa::DecArgs &a, void *ws, hipStream_t stream) {
+    if (p.headdim <= 64)
+        return p.headdim == 64 ? fa::launch_decode<DT, C, 64, true>(p, a, ws, stream)
+                               : fa::launch_decode<DT, C, 64, false>(p, a, ws, stream);
+    return p.headdim == 128 ? fa::launch_decode<DT, C, 128, true>(p, a, ws, stream)
+                            : fa::launch_decode<DT, C, 128, false>(p, a, ws, stream);
+}
+
+// Split-KV decode path (fa_decode.hpp) for few (q-head, position) rows per (batch, kv-head): the
+// reference's Sq == 1 pack and short GQA query blocks. FA_GFX950_DECODE=0 sends them to the
+// prefill kernel instead (A/B measurements).
+bool use_decode(const fa_fwd_params &p) {
+    const char *e = getenv("FA_GFX950_DECODE");
+    if (e && strcmp(e, "0") == 0) return false;
+    if (fa::variant_from_env() != 0) return false;
+    if (p.head_q_per_group * p.seqlen_q > fa::kDecMaxRows) return false;
+    // the row block's q rows are addressed by 32-bit offsets from the group's first q-head
+    const int64_t qspan = ((p.head_q_per_group - 1) * p.q_head_stride + (p.seqlen_q - 1) * p.q_seqlen_stride +
+                           p.headdim) * 2;
+    return qspan >= 0 && qspan < 0x7ff00000LL;
+}
+
+int dispatch(const fa_fwd_params *params, int dtype, int causal, void *ws, int64_t ws_bytes, void *stream) {
+    const int rc = check_params(params, dtype, causal);
+    if (rc != FA_OK) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    const fa_fwd_params &p = *params;
+    if (use_decode(p)) {
+        fa::DecArgs a = fa::decode_plan(p, ws ? fa::kDecMaxSplit : 1);
+        if (ws && fa::decode_ws_bytes(p, a) > ws_bytes)
+            return set_err(FA_ERR_INVALID_ARGUMENT, "workspace of %lld bytes is smaller than the %lld required",
+                           (long long)ws_bytes, (long long)fa::decode_ws_bytes(p, a));
+        if (dtype == FA_DTYPE_F16)
+            return causal ? launch_dec<fa::F16, true>(p, a, ws, s) : launch_dec<fa::F16, false>(p, a, ws, s);
+        return causal ? launch_dec<fa::BF16, true>(p, a, ws, s) : launch_dec<fa::BF16, false>(p, a, ws, s);
+    }
+    if (dtype == FA_DTYPE_F16)
+        return causal ? launch<fa::F16, true>(p, s) : launch<fa::F16, false>(p, s);
+    return causal ? launch<fa::BF16, true>(p, s) : launch<fa::BF16, false>(p, s);
+}
 
 }  // namespace
 
@@ -99,12 +141,20 @@ extern "C" int fa_fwd_gfx950_check(const fa_fwd_params *params, int dtype, int c
 }
 
 extern "C" int fa_fwd_gfx950(const fa_fwd_params *params, int dtype, int causal, void *stream) {
-    const int rc = check_params(params, dtype, causal);
-    if (rc != FA_OK) return rc;
-    hipStream_t s = (hipStream_t)stream;
-    if (dtype == FA_DTYPE_F16)
-        return causal ? launch<fa::F16, true>(*params, s) : launch<fa::F16, false>(*params, s);
-    return causal ? launch<fa::BF16, true>(*params, s) : launch<fa::BF16, false>(*params, s);
+    return dispatch(params, dtype, causal, nullptr, 0, stream);
+}
+
+extern "C" int64_t fa_fwd_gfx950_workspace_size(const fa_fwd_params *params, int dtype, int causal) {
+    if (check_params(params, dtype, causal) != FA_OK) return -1;
+    if (!use_decode(*params)) return 0;
+    return fa::decode_ws_bytes(*params, fa::decode_plan(*params, fa::kDecMaxSplit));
+}
+
+extern "C" int fa_fwd_gfx950_ws(const fa_fwd_params *params, int dtype, int causal, void *workspace,
+                                int64_t workspace_bytes, void *stream) {
+    if (workspace && ((uintptr_t)workspace & 15))
+        return set_err(FA_ERR_INVALID_ARGUMENT, "workspace must be 16-byte aligned");
+    return dispatch(params, dtype, causal, workspace_bytes > 0 ? workspace : nullptr, workspace_bytes, stream);
 }
 
 extern "C" const char *fa_last_error(void) { return g_err; }
@@ -115,6 +165,15 @@ extern "C" int fa_fwd_gfx950_geometry(const fa_fwd_params *params, int causal, i
                                       int64_t *block_n, int64_t *threads, int64_t *workgroups) {
     (void)causal;
     if (!params) return set_err(FA_ERR_INVALID_ARGUMENT, "params is NULL");
+    if (use_decode(*params)) {
+        // without a workspace fa_fwd_gfx950 runs the decode kernel unsplit
+        const fa::DecArgs a = fa::decode_plan(*params, 1);
+        if (block_m) *block_m = fa::kDecRows;
+        if (block_n) *block_n = fa::kDecKeys;
+        if (threads) *threads = fa::kDecWaves * 64;
+        if (workgroups) *workgroups = fa::decode_units(*params, a) * a.n_split;
+        return FA_OK;
+    }
     const int64_t n_qtiles = (params->seqlen_q + fa::kBlockM - 1) / fa::kBlockM;
     if (block_m) *block_m = fa::kBlockM;
     if (block_n) *block_n = fa::kBlockN;

@@ -2,6 +2,7 @@
 // per combination of FA_INST_DT (F16 | BF16), FA_INST_CAUSAL (0 | 1), FA_INST_D (64 | 128) and
 // FA_INST_EXACT (0 | 1), in parallel, and links the objects with fa_fwd_gfx950.hip.
 #include "fa_fwd_kernels.hpp"
+#include "fa_decode.hpp"
 
 #if !defined(FA_INST_DT) || !defined(FA_INST_CAUSAL) || !defined(FA_INST_D) || !defined(FA_INST_EXACT)
 #error "fa_inst.hip needs -DFA_INST_DT= -DFA_INST_CAUSAL= -DFA_INST_D= -DFA_INST_EXACT="
@@ -10,4 +11,7 @@
 namespace fa {
 template int launch_one<FA_INST_DT, (FA_INST_CAUSAL != 0), FA_INST_D, (FA_INST_EXACT != 0)>(const fa_fwd_params &,
                                                                                         hipStream_t);
+template int launch_decode<FA_INST_DT, (FA_INST_CAUSAL != 0), FA_INST_D, (FA_INST_EXACT != 0)>(const fa_fwd_params &,
+                                                                                           DecArgs, void *,
+                                                                                           hipStream_t);
 }  // namespace fa

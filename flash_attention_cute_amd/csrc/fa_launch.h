@@ -4,6 +4,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -40,6 +41,62 @@ unsigned long long *stamp_buffer();
 template <class DT, bool C, int kD, bool kExact>
 int launch_one(const fa_fwd_params &p, hipStream_t stream);
 
+
+// ---- split-KV decode (fa_decode.hpp) -------------------------------------------------------------
+constexpr int kDecRows = 32;  // query rows per row block (one 32x32 MFMA column block)
+constexpr int kDecKeys = 32;  // keys per tile
+constexpr int kDecWaves = 4;  // waves per workgroup, each on its own contiguous key range
+// decode kernel when a (batch, kv-head) has at most this many (q-head, position) rows
+constexpr int kDecMaxRows = 2 * kDecRows;
+// split plan: about one workgroup per CU (the 128 KiB LDS ring admits one), every wave at least
+// kDecMinTilesPerWave tiles
+constexpr int kDecTargetWgs = 256;
+constexpr int kDecMinTilesPerWave = 4;
+constexpr int kDecMaxSplit = 64;
+
+struct DecArgs {
+    int g;          // q-heads per kv-head
+    int rows;       // g * Sq: (q-head, position) rows of one (batch, kv-head)
+    int n_rb;       // 32-row blocks per (batch, kv-head)
+    int n_split;    // key splits (workgroups per row block)
+    int tps;        // 32-key tiles per split
+    float *ws_o;    // [units * n_split][32][kD] fp32 partial O / l    (n_split > 1)
+    float *ws_lse;  // [units * n_split][32] fp32 m * s' + log2(l)      (n_split > 1)
+};
+
+inline int64_t decode_units(const fa_fwd_params &p, const DecArgs &a) {
+    return p.batch_size * p.num_heads_kv * a.n_rb;
+}
+
+inline DecArgs decode_plan(const fa_fwd_params &p, int max_split) {
+    DecArgs a{};
+    a.g = (int)p.head_q_per_group;
+    a.rows = (int)(p.head_q_per_group * p.seqlen_q);
+    a.n_rb = (a.rows + kDecRows - 1) / kDecRows;
+    const int64_t units = decode_units(p, a);
+    const int n_tiles = (int)((p.seqlen_kv + kDecKeys - 1) / kDecKeys);
+    int64_t ns = (kDecTargetWgs + units - 1) / units;
+    const int64_t by_len = n_tiles / (kDecWaves * kDecMinTilesPerWave);
+    ns = ns < by_len ? ns : by_len;
+    ns = ns < max_split ? ns : max_split;
+    ns = ns < 1 ? 1 : ns;
+    a.tps = (int)((n_tiles + ns - 1) / ns);
+    a.n_split = (n_tiles + a.tps - 1) / a.tps;
+    return a;
+}
+
+// workspace bytes of a plan (fp32 partials + lse); 0 when it does not split
+inline int64_t decode_ws_bytes(const fa_fwd_params &p, const DecArgs &a) {
+    if (a.n_split <= 1) return 0;
+    const int64_t slots = decode_units(p, a) * a.n_split * kDecRows;
+    const int64_t dpad = p.headdim <= 64 ? 64 : 128;
+    return slots * dpad * 4 + slots * 4;
+}
+
+// launch the decode kernel (+ the split combine when a.n_split > 1) of one instantiation
+template <class DT, bool C, int kD, bool kExact>
+int launch_decode(const fa_fwd_params &p, DecArgs a, void *ws, hipStream_t stream);
+
 #define FA_FOR_EACH_INSTANCE(X)                                                                    \
     X(F16, false, 64, false) X(F16, false, 64, true) X(F16, false, 128, false) X(F16, false, 128, true) \
     X(F16, true, 64, false) X(F16, true, 64, true) X(F16, true, 128, false) X(F16, true, 128, true)     \
@@ -47,7 +104,9 @@ int launch_one(const fa_fwd_params &p, hipStream_t stream);
     X(BF16, false, 128, true) X(BF16, true, 64, false) X(BF16, true, 64, true)                         \
     X(BF16, true, 128, false) X(BF16, true, 128, true)
 
-#define FA_DECLARE_EXTERN(DT, C, D, E) extern template int launch_one<DT, C, D, E>(const fa_fwd_params &, hipStream_t);
+#define FA_DECLARE_EXTERN(DT, C, D, E)                                                  \
+    extern template int launch_one<DT, C, D, E>(const fa_fwd_params &, hipStream_t);   \
+    extern template int launch_decode<DT, C, D, E>(const fa_fwd_params &, DecArgs, void *, hipStream_t);
 FA_FOR_EACH_INSTANCE(FA_DECLARE_EXTERN)
 #undef FA_DECLARE_EXTERN
 

@@ -151,8 +151,15 @@ torch::Tensor flash_attention_fwd(torch::Tensor &q, torch::Tensor &k, torch::Ten
 
     const int dtype = qx.scalar_type() == torch::kHalf ? FA_DTYPE_F16 : FA_DTYPE_BF16;
     void *stream = c10::hip::getCurrentHIPStream(qx.device().index()).stream();
-    const int rc = fa_fwd_gfx950(&params, dtype, causal ? 1 : 0, stream);
-    TORCH_CHECK(rc == FA_OK, "fa_fwd_gfx950 failed (code ", rc, "): ", fa_last_error());
+    // split-KV decode (few rows per kv-head) wants fp32 scratch for its partials: taken from
+    // torch's caching allocator on the current stream, so it is graph-capture safe and reused
+    const int64_t ws_bytes = fa_fwd_gfx950_workspace_size(&params, dtype, causal ? 1 : 0);
+    TORCH_CHECK(ws_bytes >= 0, "fa_fwd_gfx950_workspace_size failed: ", fa_last_error());
+    torch::Tensor ws;
+    if (ws_bytes > 0) ws = torch::empty({ws_bytes}, qx.options().dtype(torch::kUInt8));
+    const int rc = fa_fwd_gfx950_ws(&params, dtype, causal ? 1 : 0, ws_bytes > 0 ? ws.data_ptr() : nullptr,
+                                    ws_bytes, stream);
+    TORCH_CHECK(rc == FA_OK, "fa_fwd_gfx950_ws failed (code ", rc, "): ", fa_last_error());
 
     if (is_pack_head_q) {
         head_q = head_kv * head_q_per_group;

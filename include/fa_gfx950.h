@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define FA_GFX950_ABI_VERSION 1
+#define FA_GFX950_ABI_VERSION 2
 
 /* Field order mirrors reference csrc/flash_attention.h:5-37. */
 typedef struct fa_fwd_params {
@@ -98,6 +98,25 @@ enum {
  * csrc/kernel_dispatcher.h:20-52.
  */
 int fa_fwd_gfx950(const fa_fwd_params *params, int dtype, int causal, void *stream);
+
+/*
+ * Workspace variant. Few query rows per kv-head (the Sq == 1 q-head pack of
+ * reference csrc/flash_attention_api.cpp:72-83, or head_q_per_group * Sq <=
+ * 64) run a split-KV decode kernel; splitting the keys over more workgroups
+ * needs `workspace_bytes` >= fa_fwd_gfx950_workspace_size() of device memory
+ * for fp32 partials. With workspace == NULL it behaves exactly like
+ * fa_fwd_gfx950 (decode kernel unsplit). The workspace is scratch: it may be
+ * reused as soon as the launch completes in stream order. 16-byte aligned.
+ * No reference counterpart (split-KV is a TODO at reference README.md:20).
+ */
+int fa_fwd_gfx950_ws(const fa_fwd_params *params, int dtype, int causal, void *workspace,
+                     int64_t workspace_bytes, void *stream);
+
+/*
+ * Bytes of workspace fa_fwd_gfx950_ws wants for these parameters (0 when the
+ * launch does not split; -1 when the parameters are invalid). Host-only.
+ */
+int64_t fa_fwd_gfx950_workspace_size(const fa_fwd_params *params, int dtype, int causal);
 
 /*
  * Validate `params` exactly as fa_fwd_gfx950 does, without touching the

@@ -40,7 +40,8 @@ def lib():
 
 def test_header_declares_the_boundary():
     assert set(declared_functions()) == {"fa_fwd_gfx950", "fa_fwd_gfx950_check", "fa_last_error", "fa_abi_version",
-                                         "fa_fwd_gfx950_geometry"}
+                                         "fa_fwd_gfx950_geometry", "fa_fwd_gfx950_ws",
+                                         "fa_fwd_gfx950_workspace_size"}
 
 
 def test_every_declared_symbol_is_exported(lib):
@@ -80,7 +81,7 @@ def check(lib, p, dtype=0, causal=0):
 
 def test_abi_version(lib):
     lib.fa_abi_version.restype = ctypes.c_int
-    assert lib.fa_abi_version() == 1
+    assert lib.fa_abi_version() == 2
 
 
 def test_check_accepts_valid(lib):
@@ -126,3 +127,66 @@ def test_geometry(lib):
     bm, bn, thr, wg = (x.value for x in vals)
     assert (bm, bn, thr) == (256, 64, 256)  # fa_fwd_w4: 4 waves
     assert wg == 2 * 8 * ((300 + bm - 1) // bm)
+
+
+def decode_params(b=32, hq=32, hkv=8, sk=4096, d=128, sq=1, pack=True) -> FaFwdParams:
+    """Parameters as the torch host API passes them for a decode step: Sq == 1 q-heads packed into
+    the rows of one (batch, kv-head) problem (reference csrc/flash_attention_api.cpp:72-83)."""
+    g = hq // hkv
+    if pack:
+        hq, sq, g = hkv, g * sq, 1
+    p = good_params(batch_size=b, num_heads_q=hq, num_heads_kv=hkv, seqlen_q=sq, seqlen_kv=sk, headdim=d,
+                    head_q_per_group=g)
+    for t, h, s in (("q", hq, sq), ("k", hkv, sk), ("v", hkv, sk), ("o", hq, sq)):
+        setattr(p, f"{t}_batch_stride", h * s * d)
+        setattr(p, f"{t}_head_stride", s * d)
+        setattr(p, f"{t}_seqlen_stride", d)
+    return p
+
+
+def geometry(lib, p):
+    lib.fa_fwd_gfx950_geometry.restype = ctypes.c_int
+    vals = [ctypes.c_int64() for _ in range(4)]
+    assert lib.fa_fwd_gfx950_geometry(ctypes.byref(p), 0, *[ctypes.byref(x) for x in vals]) == FA_OK
+    return tuple(x.value for x in vals)
+
+
+def ws_size(lib, p, dtype=0, causal=0):
+    lib.fa_fwd_gfx950_workspace_size.restype = ctypes.c_int64
+    return lib.fa_fwd_gfx950_workspace_size(ctypes.byref(p), dtype, causal)
+
+
+def test_decode_geometry_and_workspace(lib):
+    # B32 x Hkv8 = 256 row blocks already fill the chip: one workgroup each, no split, no workspace
+    p = decode_params()
+    assert geometry(lib, p) == (32, 32, 256, 256)
+    assert ws_size(lib, p) == 0
+    # batch 1: 8 row blocks, split over the keys -> fp32 partials (32 rows x 128) + lse per split
+    p1 = decode_params(b=1, sk=32768)
+    n = ws_size(lib, p1)
+    assert n > 0 and n % (8 * 32 * (128 * 4 + 4)) == 0
+    splits = n // (8 * 32 * (128 * 4 + 4))
+    assert 2 <= splits <= 64
+    # short K/V: no split (every wave keeps >= 4 tiles of 32 keys)
+    assert ws_size(lib, decode_params(b=1, sk=256)) == 0
+    # prefill shapes need no workspace; invalid parameters report -1
+    assert ws_size(lib, good_params()) == 0
+    assert ws_size(lib, good_params(headdim=100)) == -1
+
+
+def test_decode_rows_threshold(lib):
+    # unpacked GQA with a few query positions also runs the decode kernel while g * Sq <= 64 rows
+    assert geometry(lib, decode_params(sq=8, pack=False))[0] == 32   # 4 heads x 8 positions
+    assert geometry(lib, decode_params(sq=17, pack=False))[0] == 256  # 68 rows -> prefill kernel
+
+
+def test_ws_entry_rejects_small_workspace(lib):
+    lib.fa_fwd_gfx950_ws.restype = ctypes.c_int
+    p = decode_params(b=1, sk=32768)
+    need = ws_size(lib, p)
+    rc = lib.fa_fwd_gfx950_ws(ctypes.byref(p), 0, 0, ctypes.c_void_p(0x100000), ctypes.c_int64(need - 16), None)
+    assert rc == FA_ERR_INVALID_ARGUMENT
+    lib.fa_last_error.restype = ctypes.c_char_p
+    assert b"workspace" in lib.fa_last_error()
+    rc = lib.fa_fwd_gfx950_ws(ctypes.byref(p), 0, 0, ctypes.c_void_p(0x100008), ctypes.c_int64(need), None)
+    assert rc == FA_ERR_INVALID_ARGUMENT  # misaligned
