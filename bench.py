@@ -51,6 +51,10 @@ CONFIGS = {
                Sq=4096, Sk=4096, D=128, dtype="bf16", causal=True),
     "decode": dict(workload="decode GQA fp16 B32 Hq32 Hkv8 Sq1 Sk4096 D128 (q-head pack)", B=32, Hq=32,
                    Hkv=8, Sq=1, Sk=4096, D=128, dtype="fp16", causal=False),
+    # long-context decode at batch 1: the same K/V bytes as "decode" in 8 (batch, kv-head) streams,
+    # split over the keys (split-KV + combine)
+    "decode_long": dict(workload="decode GQA bf16 B1 Hq32 Hkv8 Sq1 Sk131072 D128 (split-KV)", B=1, Hq=32, Hkv=8,
+                        Sq=1, Sk=131072, D=128, dtype="bf16", causal=False),
 }
 
 

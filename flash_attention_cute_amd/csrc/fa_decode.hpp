@@ -32,6 +32,16 @@
 
 namespace fa {
 
+// LDS-DMA with the non-temporal policy (K/V of a decode step are read once)
+__device__ __forceinline__ void dma_one_nt(const rsrc_t &rs, const uint32_t lds, const int voff, const bool nop) {
+    if (nop)
+        asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, 0 offen nt lds" ::"v"(voff), "s"(rs), "{m0}"(lds)
+                     : "memory");
+    else
+        asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen nt lds" ::"v"(voff), "s"(rs), "{m0}"(lds)
+                     : "memory");
+}
+
 template <int kD>
 struct DecGeo {
     using G = Geo<kD>;
@@ -109,10 +119,17 @@ __global__ __launch_bounds__(256, 1) void fa_decode(const fa_fwd_params p, const
         const uint32_t dst = ring_u + (t & 1) * DG::kSlot;
         const rsrc_t kr = make_rsrc(kb + 2 * (int64_t)key0 * ks_, slab_bytes(rows, ks_, D));
         const rsrc_t vr = make_rsrc(vb + 2 * (int64_t)key0 * vs_, slab_bytes(rows, vs_, D));
+        if (a.flags & kDecNt) {
 #pragma unroll
-        for (int n = 0; n < NP; ++n) dma_one(kr, dst + n * 1024, kvo[n], n == 0);
+            for (int n = 0; n < NP; ++n) dma_one_nt(kr, dst + n * 1024, kvo[n], n == 0);
 #pragma unroll
-        for (int n = 0; n < NP; ++n) dma_one(vr, dst + DG::kTile + n * 1024, vvo[n], n == 0);
+            for (int n = 0; n < NP; ++n) dma_one_nt(vr, dst + DG::kTile + n * 1024, vvo[n], n == 0);
+        } else {
+#pragma unroll
+            for (int n = 0; n < NP; ++n) dma_one(kr, dst + n * 1024, kvo[n], n == 0);
+#pragma unroll
+            for (int n = 0; n < NP; ++n) dma_one(vr, dst + DG::kTile + n * 1024, vvo[n], n == 0);
+        }
     };
     // ---- Q: the row block's 32 rows by LDS-DMA into a shared K-swizzled image -----------------
     // (rows are scattered over q-heads / positions; a descriptor over the group's span bounds
@@ -294,7 +311,7 @@ __global__ __launch_bounds__(256, 1) void fa_decode(const fa_fwd_params p, const
                 }
             }
         }
-    } else {
+    } else if (rg2 < a.rows) {
         const size_t slot = (size_t)blockIdx.x * kDecRows + row;  // (unit * n_split + split) * 32 + row
         float *dst = a.ws_o + slot * kD + part * DPT;
 #pragma unroll
@@ -304,50 +321,51 @@ __global__ __launch_bounds__(256, 1) void fa_decode(const fa_fwd_params p, const
     }
 }
 
-// Merge n_split partials (O / l and lse = m*s' + log2 l, log2 units) of one row block.
+// Merge n_split partials (O / l and lse = m*s' + log2 l, log2 units): one wave per (row block, row),
+// lane l owns d = 2l, 2l+1 (kD = 128) or d = l (kD = 64), so every partial row is one contiguous
+// 512 / 256-B wave read.
 template <class DT, int kD, bool kExactD>
 __global__ __launch_bounds__(256) void fa_decode_combine(const fa_fwd_params p, const DecArgs a) {
-    constexpr int DPT = kD / 8;
-    const int unit = blockIdx.x;
+    constexpr int DPL = kD / 64;  // d values per lane
+    const int wid = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int unit = wid / kDecRows, row = wid % kDecRows;
     const int rb = unit % a.n_rb;
+    const int rg = rb * kDecRows + row;
+    if (unit >= (int)(p.batch_size * p.num_heads_kv) * a.n_rb || rg >= a.rows) return;
     const int hkv = (unit / a.n_rb) % (int)p.num_heads_kv;
     const int b = unit / (a.n_rb * (int)p.num_heads_kv);
     const int Sq = (int)p.seqlen_q, D = (int)p.headdim;
-    const int row = threadIdx.x >> 3, part = threadIdx.x & 7;
-    const int rg = rb * kDecRows + row;
-    if (rg >= a.rows) return;
     const size_t base = (size_t)unit * a.n_split * kDecRows + row;
     float M = kNeg;
     for (int s = 0; s < a.n_split; ++s) M = fmaxf(M, a.ws_lse[base + (size_t)s * kDecRows]);
-    float acc[DPT], L = 0.f;
+    float acc[DPL], L = 0.f;
 #pragma unroll
-    for (int i = 0; i < DPT; ++i) acc[i] = 0.f;
+    for (int i = 0; i < DPL; ++i) acc[i] = 0.f;
     for (int s = 0; s < a.n_split; ++s) {
         const size_t slot = base + (size_t)s * kDecRows;
         const float ls = a.ws_lse[slot];
         const float w = (ls <= 0.5f * kNeg) ? 0.f : __builtin_amdgcn_exp2f(ls - M);
         L += w;
-        const float *src = a.ws_o + slot * kD + part * DPT;
-#pragma unroll
-        for (int i = 0; i < DPT; i += 4) {
-            const float4 x = *(const float4 *)(src + i);
-            acc[i] += w * x.x;
-            acc[i + 1] += w * x.y;
-            acc[i + 2] += w * x.z;
-            acc[i + 3] += w * x.w;
+        const float *src = a.ws_o + slot * kD + lane * DPL;
+        if constexpr (DPL == 2) {
+            const float2 x = *(const float2 *)src;
+            acc[0] += w * x.x;
+            acc[1] += w * x.y;
+        } else {
+            acc[0] += w * src[0];
         }
     }
     const float inv = L > 0.f ? 1.f / L : 0.f;
     const int hq = hkv * a.g + rg / Sq, pos = rg % Sq;
     char *orow = (char *)p.o_ptr +
                  2 * ((int64_t)b * p.o_batch_stride + (int64_t)hq * p.o_head_stride + (int64_t)pos * p.o_seqlen_stride);
-#pragma unroll
-    for (int i = 0; i < DPT; i += 8) {
-        const int d = part * DPT + i;
-        if (kExactD || d < D) {
-            const u32x4 w4 = {DT::pack(acc[i] * inv, acc[i + 1] * inv), DT::pack(acc[i + 2] * inv, acc[i + 3] * inv),
-                              DT::pack(acc[i + 4] * inv, acc[i + 5] * inv), DT::pack(acc[i + 6] * inv, acc[i + 7] * inv)};
-            *(u32x4 *)(orow + 2 * d) = w4;
+    const int d = lane * DPL;
+    if (kExactD || d < D) {
+        if constexpr (DPL == 2) {
+            *(uint32_t *)(orow + 2 * d) = DT::pack(acc[0] * inv, acc[1] * inv);
+        } else {
+            const uint32_t w2 = DT::pack(acc[0] * inv, 0.f);
+            *(uint16_t *)(orow + 2 * d) = (uint16_t)(w2 & 0xffff);
         }
     }
 }
@@ -362,7 +380,8 @@ int launch_decode(const fa_fwd_params &p, DecArgs a, void *ws, hipStream_t strea
     }
     hipLaunchKernelGGL((fa_decode<DT, C, kD, kExact>), dim3((uint32_t)(units * a.n_split)), dim3(256), 0, stream, p, a);
     if (a.n_split > 1)
-        hipLaunchKernelGGL((fa_decode_combine<DT, kD, kExact>), dim3((uint32_t)units), dim3(256), 0, stream, p, a);
+        hipLaunchKernelGGL((fa_decode_combine<DT, kD, kExact>), dim3((uint32_t)(units * kDecRows / 4)), dim3(256), 0,
+                           stream, p, a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "HIP launch failed: %s", hipGetErrorString(e));
     return FA_OK;

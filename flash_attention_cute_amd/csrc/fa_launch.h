@@ -62,7 +62,9 @@ struct DecArgs {
     int tps;        // 32-key tiles per split
     float *ws_o;    // [units * n_split][32][kD] fp32 partial O / l    (n_split > 1)
     float *ws_lse;  // [units * n_split][32] fp32 m * s' + log2(l)      (n_split > 1)
+    int flags;      // kDec* bits
 };
+constexpr int kDecNt = 1;  // K/V LDS-DMA with the non-temporal cache policy
 
 inline int64_t decode_units(const fa_fwd_params &p, const DecArgs &a) {
     return p.batch_size * p.num_heads_kv * a.n_rb;
@@ -75,7 +77,11 @@ inline DecArgs decode_plan(const fa_fwd_params &p, int max_split) {
     a.n_rb = (a.rows + kDecRows - 1) / kDecRows;
     const int64_t units = decode_units(p, a);
     const int n_tiles = (int)((p.seqlen_kv + kDecKeys - 1) / kDecKeys);
-    int64_t ns = (kDecTargetWgs + units - 1) / units;
+    const char *tw = getenv("FA_DEC_TARGET_WGS");  // tuning knob (A/B runs)
+    const int64_t target = tw ? atoll(tw) : kDecTargetWgs;
+    const char *fl = getenv("FA_DEC_FLAGS");
+    a.flags = fl ? atoi(fl) : kDecNt;
+    int64_t ns = (target + units - 1) / units;
     const int64_t by_len = n_tiles / (kDecWaves * kDecMinTilesPerWave);
     ns = ns < by_len ? ns : by_len;
     ns = ns < max_split ? ns : max_split;

@@ -9,14 +9,18 @@ import collections
 import csv
 import glob
 import json
+import os
 import sys
+
+# kernels whose dispatches are averaged (the dominant kernel of the config)
+KERNELS = os.environ.get("PMC_KERNELS", "fa::fa_fwd,fa::fa_decode<").split(",")
 
 src, cfg, out = sys.argv[1], sys.argv[2], sys.argv[3]
 note = sys.argv[4] if len(sys.argv) > 4 else src
 agg = collections.defaultdict(list)
 for f in glob.glob(f"{src}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "fa::fa_fwd" in r["Kernel_Name"]:
+        if any(k in r["Kernel_Name"] for k in KERNELS):
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
 mean = {k: sum(v) / len(v) for k, v in agg.items()}
 res = {"config": cfg, "source": note, "dispatches": {k: len(v) for k, v in agg.items()},
