@@ -73,7 +73,8 @@ def _jobs() -> int:
     return max(1, min(int(n), 16))
 
 
-def build_abi(force: bool = False, verbose: bool = False, stamps: bool = False) -> Path:
+def build_abi(force: bool = False, verbose: bool = False, stamps: bool = False, tag: str = "",
+              defines: tuple = (), flags: tuple = (), only: tuple = ()) -> Path:
     """Compile the HIP kernels + C-ABI into lib/libfa_gfx950.so (gfx950 code objects).
 
     Each kernel instantiation is its own translation unit (csrc/fa_inst.hip with -D selectors), so
@@ -81,22 +82,26 @@ def build_abi(force: bool = False, verbose: bool = False, stamps: bool = False) 
     """
     from concurrent.futures import ThreadPoolExecutor
 
-    out_lib = ROOT / "build" / "stamps" / "libfa_gfx950.so" if stamps else ABI_LIB
+    # diagnostic builds (stamps, experiments) go to build/stamps[_<tag>]/, never over the product
+    sdir = "stamps" + (f"_{tag}" if tag else "")
+    out_lib = ROOT / "build" / sdir / "libfa_gfx950.so" if stamps else ABI_LIB
     out_lib.parent.mkdir(parents=True, exist_ok=True)
     if not force and not _stale(out_lib, abi_sources()):
         return out_lib
     if not HIPCC.exists():
         raise RuntimeError(f"hipcc not found at {HIPCC}")
-    objdir = ROOT / "build" / ("obj_stamps" if stamps else "obj")
-    extra = ["-DFA_STAMPS=1"] if stamps else []
+    objdir = ROOT / "build" / (f"obj_{sdir}" if stamps else "obj")
+    extra = (["-DFA_STAMPS=1"] + [f"-D{d}" for d in defines] + list(flags)) if stamps else []
     objdir.mkdir(parents=True, exist_ok=True)
     cmds = []
     objs = []
     for dt, c, d, e in INSTANCES:
         obj = objdir / f"fa_inst_{dt.lower()}_c{c}_d{d}_x{e}.o"
         objs.append(obj)
-        cmds.append([HIPCC, *HIP_FLAGS, *extra, f"-I{INCLUDE}", f"-I{CSRC}", f"-DFA_INST_DT={dt}", f"-DFA_INST_CAUSAL={c}",
-                     f"-DFA_INST_D={d}", f"-DFA_INST_EXACT={e}", "-c", CSRC / "fa_inst.hip", "-o", obj])
+        stub = ["-DFA_INST_STUB=1"] if only and (dt, c, d, e) not in only else []
+        cmds.append([HIPCC, *HIP_FLAGS, *extra, *stub, f"-I{INCLUDE}", f"-I{CSRC}", f"-DFA_INST_DT={dt}",
+                     f"-DFA_INST_CAUSAL={c}", f"-DFA_INST_D={d}", f"-DFA_INST_EXACT={e}", "-c", CSRC / "fa_inst.hip",
+                     "-o", obj])
     disp = objdir / "fa_fwd_gfx950.o"
     objs.append(disp)
     cmds.append([HIPCC, *HIP_FLAGS, *extra, f"-I{INCLUDE}", f"-I{CSRC}", "-c", CSRC / "fa_fwd_gfx950.hip", "-o", disp])

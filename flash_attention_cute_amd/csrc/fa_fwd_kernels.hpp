@@ -86,6 +86,14 @@ struct F16 {
         f16x2 v = __builtin_convertvector((f32x2){lo, hi}, f16x2);
         return __builtin_bit_cast(uint32_t, v);
     }
+    // 8 values * s in fp32, rounded back (RNE)
+    static __device__ __forceinline__ u32x4 scale8(u32x4 v, float s) {
+        const f16x8 x = __builtin_bit_cast(f16x8, v);
+        u32x4 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[i] = pack((float)x[2 * i] * s, (float)x[2 * i + 1] * s);
+        return r;
+    }
 };
 
 struct BF16 {
@@ -98,6 +106,13 @@ struct BF16 {
     static __device__ __forceinline__ uint32_t pack(float lo, float hi) {
         bf16x2 v = __builtin_convertvector((f32x2){lo, hi}, bf16x2);
         return __builtin_bit_cast(uint32_t, v);
+    }
+    static __device__ __forceinline__ u32x4 scale8(u32x4 v, float s) {
+        const bf16x8 x = __builtin_bit_cast(bf16x8, v);
+        u32x4 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[i] = pack((float)x[2 * i] * s, (float)x[2 * i + 1] * s);
+        return r;
     }
 };
 
@@ -512,6 +527,7 @@ __device__ __forceinline__ void agpr_mfma(const u32x4 &a, const u32x4 &b) {
         else fa_agpr_mfma_bf16_##N(a, b);                             \
     }
     FA_CASE(0) FA_CASE(16) FA_CASE(32) FA_CASE(48) FA_CASE(64) FA_CASE(80) FA_CASE(96) FA_CASE(112)
+    FA_CASE(192) FA_CASE(208)
 #undef FA_CASE
 }
 template <int DTL, bool kBlockB>
@@ -545,6 +561,8 @@ __device__ __forceinline__ float agpr_read1() {
     if constexpr (BASE == 64) return fa_agpr_read1_64();
     else if constexpr (BASE == 80) return fa_agpr_read1_80();
     else if constexpr (BASE == 128) return fa_agpr_read1_128();
+    else if constexpr (BASE == 192) return fa_agpr_read1_192();
+    else if constexpr (BASE == 208) return fa_agpr_read1_208();
     else return fa_agpr_read1_144();
 }
 
@@ -567,6 +585,15 @@ template <int QB>
 __device__ __forceinline__ void agpr_qset(const u32x4 &v) {
 #define FA_CASE(N) \
     if constexpr (QB == N) fa_agpr_qset_##N(v[0], v[1], v[2], v[3]);
+    FA_CASE(128) FA_CASE(132) FA_CASE(136) FA_CASE(140) FA_CASE(144) FA_CASE(148) FA_CASE(152) FA_CASE(156)
+    FA_CASE(160) FA_CASE(164) FA_CASE(168) FA_CASE(172) FA_CASE(176) FA_CASE(180) FA_CASE(184) FA_CASE(188)
+#undef FA_CASE
+}
+// first k-step with C = bias (the running reference max, kFoldScale)
+template <bool kF16, int QB>
+__device__ __forceinline__ void mfma_sq_bias(f32x16 &acc, const u32x4 &a, const f32x16 &bias) {
+#define FA_CASE(N) \
+    if constexpr (QB == N) { if constexpr (kF16) fa_sq_f16_##N##_b(acc, a, bias); else fa_sq_bf16_##N##_b(acc, a, bias); }
     FA_CASE(128) FA_CASE(132) FA_CASE(136) FA_CASE(140) FA_CASE(144) FA_CASE(148) FA_CASE(152) FA_CASE(156)
     FA_CASE(160) FA_CASE(164) FA_CASE(168) FA_CASE(172) FA_CASE(176) FA_CASE(180) FA_CASE(184) FA_CASE(188)
 #undef FA_CASE
@@ -663,6 +690,23 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #endif
     using G = Geo<kD>;
     constexpr bool F = DT::kIsF16;
+#ifndef FA_FOLD
+    constexpr bool kFold = false;
+#else
+    // (experiment, off: +32 VGPRs of bias push the kernel past 256 arch VGPRs and it measured
+    // slower) Q is pre-scaled by s' = scale*log2(e) (fp32 multiply, rounded to T once per workgroup) and
+    // the first k-step of S = K.Q^T accumulates from C = -m*s' (the running reference max,
+    // "bias"): S is then already the exp2 argument and a score costs no fma
+    constexpr bool kFold = true;
+#endif
+#ifndef FA_LSUM
+    constexpr bool kLsum = false;
+#else
+    // (experiment, off: phase 2 turns MFMA-bound, +2.7% cycles measured) row sums of P by one
+    // extra MFMA per (block, 16-key step) with an all-ones A operand, into a[192 + 16X]: 8 MFMAs
+    // per tile instead of 64 VALU adds
+    constexpr bool kLsum = true;
+#endif
     constexpr int KS = G::kKSteps;
     constexpr int DTL = G::kDTiles;
     constexpr int RB = G::kRowBytes;
@@ -730,6 +774,10 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                 qv[X * KS + ks] = __builtin_amdgcn_raw_buffer_load_b128(
                     qr, ok ? (32 * X + r) * qs * 2 + 32 * ks + 16 * h : 0x7ffffff0, 0, 0);
             }
+        if constexpr (kFold) {
+#pragma unroll
+            for (int i = 0; i < 2 * KS; ++i) qv[i] = DT::scale8(qv[i], sc);
+        }
         static_for<2 * KS>([&](auto I) { agpr_qset<QB + 4 * decltype(I)::value>(qv[decltype(I)::value]); });
     }
 
@@ -773,11 +821,18 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         float mE, mO;         // two max chains over the tile being reduced (mE then holds m_new)
         float l, t;           // this lane's half of the row sum over finished tiles; s0 sum of the
                               // tile being reduced (new scale, folded into l at the rescale)
-        bool resc;
+        float delta;          // kFold: rise of the reference m*sc at this tile's decision
+        bool resc, seen, vis; // kFold: the row has seen a visible key; this tile has one
     };
     Sm st[2];
 #pragma unroll
-    for (int X = 0; X < 2; ++X) st[X] = {kNeg, 0.f, 1.f, kNeg, kNeg, 0.f, 0.f, false};
+    for (int X = 0; X < 2; ++X) st[X] = {kNeg, 0.f, 1.f, kNeg, kNeg, 0.f, 0.f, 0.f, false, false, false};
+    f32x16 bias[2];  // kFold: -m*s' per lane, the C operand of the first S k-step
+#pragma unroll
+    for (int X = 0; X < 2; ++X) bias[X] = (f32x16){};
+    const uint32_t one2 = F ? 0x3C003C00u : 0x3F803F80u;
+    const u32x4 ones = {one2, one2, one2, one2};  // kLsum: A operand of the row-sum MFMA
+    if constexpr (kLsum) fa_agpr_zero_l();
     f32x16 S[2][4];  // [tile parity][2 * block + half]: half 0 = keys 0-31, 1 = keys 32-63
     u32x4 P[2][8];   // [tile parity][4 * block + k-step]
     if constexpr (DTL == 4) fa_agpr_zero_4(); else fa_agpr_zero_2();
@@ -791,8 +846,34 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         pin(mm);
     };
     // the rescale decision of block X in two units: the row max and m_new; then m*sc and alpha
-    auto u_dec = [&](const int X, const int k) {
+    auto u_dec = [&](const int c, const int X, const int k) {
         Sm &Z = st[X];
+        if constexpr (kFold) {
+            // S already holds s*s' - m*s' (bias): the tile max is the rise over the reference
+            if (k == 0) {
+                const float mx = pair_max(fmaxf(Z.mE, Z.mO));
+                Z.vis = mx > 0.5f * kNeg;
+                const bool grow = Z.seen ? (mx > kRescaleThr) : Z.vis;
+                Z.resc = __builtin_amdgcn_ballot_w64(grow) != 0;
+                // first visible key: the reference jumps to the tile max (any sign); later only up
+                Z.delta = Z.resc ? (Z.seen ? fmaxf(mx, 0.f) : (Z.vis ? mx : 0.f)) : 0.f;
+                pin(Z.delta);
+            } else {
+                Z.alpha = Z.resc ? (Z.seen ? __builtin_amdgcn_exp2f(-Z.delta) : 0.f) : 1.f;
+                Z.seen = Z.seen || Z.vis;
+                pin(Z.alpha);
+                if (Z.resc) {  // rare: shift this tile's scores and the bias to the new reference
+                    Z.msc += Z.delta;
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        S[c][2 * X][i] -= Z.delta;
+                        S[c][2 * X + 1][i] -= Z.delta;
+                        bias[X][i] = -Z.msc;
+                    }
+                }
+            }
+            return;
+        }
         if (k == 0) {
             const float mx = pair_max(fmaxf(Z.mE, Z.mO));
             Z.resc = __builtin_amdgcn_ballot_w64(mx > Z.m + thr_raw) != 0;
@@ -812,7 +893,24 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // P = exp2(s * sc - m * sc) of score v of half hf of block X, in place
     auto u_exp = [&](const int c, const int X, const int hf, const int v) {
         f32x16 &s = S[c][2 * X + hf];
-        float x = __builtin_amdgcn_exp2f(__builtin_fmaf(s[v], sc, -st[X].msc));
+#if defined(FA_EXP_NOEXP)
+        float x = __builtin_fmaf(s[v], sc, -st[X].msc);
+#else
+        float x = kFold ? __builtin_amdgcn_exp2f(s[v]) : __builtin_amdgcn_exp2f(__builtin_fmaf(s[v], sc, -st[X].msc));
+#endif
+        pin(x);
+        s[v] = x;
+    };
+    // u_exp in two halves (the fma one MFMA gap ahead of the exp)
+    auto u_fma = [&](const int c, const int X, const int hf, const int v) {
+        f32x16 &s = S[c][2 * X + hf];
+        float x = __builtin_fmaf(s[v], sc, -st[X].msc);
+        pin(x);
+        s[v] = x;
+    };
+    auto u_ex2 = [&](const int c, const int X, const int hf, const int v) {
+        f32x16 &s = S[c][2 * X + hf];
+        float x = __builtin_amdgcn_exp2f(s[v]);
         pin(x);
         s[v] = x;
     };
@@ -820,9 +918,11 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // P.V operand of its 16-key k-step
     auto u_fin = [&](const int c, const int X, const int hf, const int v) {
         const f32x16 &s = S[c][2 * X + hf];
-        float &acc = hf ? st[X].l : st[X].t;
-        acc = (hf == 0 && v == 0) ? s[0] : acc + s[v];
-        pin(acc);
+        if constexpr (!kLsum) {
+            float &acc = hf ? st[X].l : st[X].t;
+            acc = (hf == 0 && v == 0) ? s[0] : acc + s[v];
+            pin(acc);
+        }
         if (v & 1) {
             uint32_t w = DT::pack(s[v - 1], s[v]);
             pin(w);
@@ -830,10 +930,18 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         }
     };
     auto rescale = [&]() {
-        if (st[0].resc) agpr_scale<DTL, false>(st[0].alpha);
-        if (st[1].resc) agpr_scale<DTL, true>(st[1].alpha);
+        if (st[0].resc) {
+            agpr_scale<DTL, false>(st[0].alpha);
+            if constexpr (kLsum) fa_agpr_scale1_192(st[0].alpha);
+        }
+        if (st[1].resc) {
+            agpr_scale<DTL, true>(st[1].alpha);
+            if constexpr (kLsum) fa_agpr_scale1_208(st[1].alpha);
+        }
+        if constexpr (!kLsum) {
 #pragma unroll
-        for (int X = 0; X < 2; ++X) st[X].l = __builtin_fmaf(st[X].l, st[X].alpha, st[X].t);
+            for (int X = 0; X < 2; ++X) st[X].l = __builtin_fmaf(st[X].l, st[X].alpha, st[X].t);
+        }
     };
 
     // ---- phase 1: S[c] = K.Q^T for both blocks (4*KS single MFMAs) ----------------------------
@@ -853,7 +961,11 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             constexpr int ks = g >> 2, i = g & 3, cb = ks & 1;
             // one counted wait per k-step (its two K fragments were read a whole k-step ahead)
             if constexpr (ks > 0 && i == 0) __builtin_amdgcn_s_waitcnt(kLgkm0);
-            mfma_sq<F, QB + 4 * ((i >> 1) * KS + ks)>(ks == 0, S[c][i], kf[cb][i & 1]);
+            if constexpr (kFold && ks == 0) mfma_sq_bias<F, QB + 4 * ((i >> 1) * KS + ks)>(S[c][i], kf[cb][i & 1], bias[i >> 1]);
+            else mfma_sq<F, QB + 4 * ((i >> 1) * KS + ks)>(ks == 0, S[c][i], kf[cb][i & 1]);
+            // the MFMA alone in its scheduling region: the pre-RA scheduler would otherwise hoist
+            // this gap's (independent) VALU above it, into the previous gap
+            FA_SCHED_FENCE();
             if constexpr (ks + 1 < KS && i == 0) {
                 kf[cb ^ 1][0] = *(const u32x4 *)(K + k_addr[ks + 1]);
                 kf[cb ^ 1][1] = *(const u32x4 *)(K + 32 * RB + k_addr[ks + 1]);
@@ -863,6 +975,22 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                 else dma_one(vr, v_lds + (ks - NP) * 1024, vvo[ks - NP], ks == NP);
             }
             if constexpr (do_sm) {
+#if defined(FA_EXP_PREFMA)
+                // fma of the next gap's units one gap ahead: no fma -> exp dependency inside a gap
+                constexpr int UPG = 32 / G1;
+                static_for<32>([&](auto U) {
+                    constexpr int u = decltype(U)::value;
+                    if constexpr (g == 0 && u < UPG) u_fma(pr, u & 1, 1, u >> 1);
+                    if constexpr (u / UPG == g + 1) u_fma(pr, u & 1, 1, u >> 1);
+                });
+                static_for<32>([&](auto U) {
+                    constexpr int u = decltype(U)::value;
+                    if constexpr (u / UPG == g) {
+                        u_ex2(pr, u & 1, 1, u >> 1);
+                        if constexpr (u >= 2) u_fin(pr, u & 1, 1, (u >> 1) - 1);
+                    }
+                });
+#else
                 static_for<32>([&](auto U) {
                     constexpr int u = decltype(U)::value;
                     if constexpr ((u * G1) / 32 == g) {
@@ -870,6 +998,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                         if constexpr (u >= 2) u_fin(pr, u & 1, 1, (u >> 1) - 1);
                     }
                 });
+#endif
             }
             FA_SCHED_FENCE();
         });
@@ -893,7 +1022,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // ---- phase 2: O^T += V^T.P^T for both blocks (8*DTL single MFMAs into the AGPRs) ----------
     // gap g (kk = g / 2DTL, i = g % 2DTL; MFMA: block i / DTL, d-tile i % DTL): V^T read i of
     // k-step kk+1, and with SM1 the first softmax half of the tile of parity cs (schedule below).
-    constexpr int G2 = 8 * DTL;
+    constexpr int NPK = 2 * DTL + (kLsum ? 2 : 0);  // MFMAs per 16-key step (+ the row-sum MFMAs)
+    constexpr int G2 = 4 * NPK;
     constexpr int GQ = G2 / 8;  // 4 (D=128) / 2 (D=64)
     // exp unit e (0..31) -> block / score: A0..A4, then B and A alternating, then B11..B15
     struct Ex {  // exp unit e (0..31) -> block / score: A0..A4, then B and A alternating, then B11..B15
@@ -930,11 +1060,14 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         for (int n = 0; n < 2 * DTL; ++n) rd(0, n, va[0]);
         static_for<G2>([&](auto G) {
             constexpr int g = decltype(G)::value;
-            constexpr int kk = g / (2 * DTL), i = g % (2 * DTL), X = i / DTL, dt = i % DTL;
+            constexpr int kk = g / NPK, i = g % NPK;
+            constexpr int X = kLsum ? i / (DTL + 1) : i / DTL, dt = kLsum ? i % (DTL + 1) : i % DTL;
             // one counted wait per 16-key step: its V^T fragments were read in the first DTL gaps
             // of the previous step, two per gap
             if constexpr (kk > 0 && i == 0) __builtin_amdgcn_s_waitcnt(kLgkm0);
-            agpr_mfma<F, X * 16 * DTL + 16 * dt>(va[kk & 1][dt], P[cp][4 * X + kk]);
+            if constexpr (dt == DTL) agpr_mfma<F, 192 + 16 * X>(ones, P[cp][4 * X + kk]);  // row sums
+            else agpr_mfma<F, X * 16 * DTL + 16 * dt>(va[kk & 1][dt], P[cp][4 * X + kk]);
+            FA_SCHED_FENCE();  // (see phase 1)
             if constexpr (kk + 1 < 4 && i < DTL) {
                 rd(kk + 1, 2 * i, va[(kk + 1) & 1]);
                 rd(kk + 1, 2 * i + 1, va[(kk + 1) & 1]);
@@ -946,7 +1079,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                 });
                 static_for<4>([&](auto K2) {
                     constexpr int X2 = decltype(K2)::value >> 1, k = decltype(K2)::value & 1;
-                    if constexpr (Ex::dec_gap(X2, k) == g) u_dec(X2, k);
+                    if constexpr (Ex::dec_gap(X2, k) == g) u_dec(cs, X2, k);
                 });
                 static_for<32>([&](auto E) {
                     constexpr int e = decltype(E)::value;
@@ -969,8 +1102,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         static_for<2>([&](auto XX) {
             constexpr int X = decltype(XX)::value;
             static_for<16>([&](auto M) { u_max(c, X, decltype(M)::value); });
-            u_dec(X, 0);
-            u_dec(X, 1);
+            u_dec(c, X, 0);
+            u_dec(c, X, 1);
             static_for<16>([&](auto VV) {
                 u_exp(c, X, 0, decltype(VV)::value);
                 u_fin(c, X, 0, decltype(VV)::value);
@@ -1026,9 +1159,20 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         const rsrc_t vr = make_rsrc(vp, tile_bytes(j * kBlockN, full_v, vs_));
         kp += step_k;
         vp += step_v;
+        // FA_EXP_*: timing experiments of the stamps build only (results are garbage)
+#if defined(FA_EXP_NOSM)
+        phase1(lds + KV0 + c * T, PAR, IC<0>{}, IC<1>{}, kr, vr, lds_base + pr * T, lds_base + (2 + c) * T);
+#elif defined(FA_EXP_NODMA)
+        phase1(lds + KV0 + c * T, PAR, IC<1>{}, IC<0>{}, kr, vr, lds_base + pr * T, lds_base + (2 + c) * T);
+#else
         phase1(lds + KV0 + c * T, PAR, IC<1>{}, IC<1>{}, kr, vr, lds_base + pr * T, lds_base + (2 + c) * T);
+#endif
         FA_STAMP(sb);
+#if defined(FA_EXP_NOSM)
+        phase2(lds + KV0 + (2 + pr) * T, IC<pr>{}, PAR, IC<0>{});
+#else
         phase2(lds + KV0 + (2 + pr) * T, IC<pr>{}, PAR, IC<1>{});
+#endif
         rescale();
         FA_STAMP(sc_);
         dma_wait();  // K_{j+1}, V_j landed
@@ -1098,7 +1242,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     mfma_drain();  // last asm MFMA -> AGPR reads
     const int os_ = (int)p.o_seqlen_stride;
     const rsrc_t orr = make_rsrc(ob + 2 * (int64_t)mw * os_, slab_bytes(min(Sq - mw, 64), os_, D));
-    auto store_block = [&](const int row, auto OBASE, const float l_lane) {
+    auto store_block = [&](const int row, auto OBASE, const float l_tot) {
         constexpr int ob0 = decltype(OBASE)::value;
         f32x16 o[DTL];
         o[0] = agpr_read16<ob0>();
@@ -1107,7 +1251,6 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             o[2] = agpr_read16<ob0 + 32>();
             o[3] = agpr_read16<ob0 + 48>();
         }
-        const float l_tot = pair_sum(l_lane);
         const float inv = (l_tot == 0.f) ? 1.f : 1.f / l_tot;
         const int orow = row * os_ * 2;
 #pragma unroll
@@ -1128,8 +1271,11 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         }
     };
     FA_STAMP(s_masked_end);
-    store_block(r, IC<0>{}, st[0].l);
-    store_block(r + 32, IC<16 * DTL>{}, st[1].l);
+    // row sums: the MFMA accumulators hold the full sum (both lane halves); the VALU path sums half
+    const float l0 = kLsum ? agpr_read1<192>() : pair_sum(st[0].l);
+    const float l1 = kLsum ? agpr_read1<208>() : pair_sum(st[1].l);
+    store_block(r, IC<0>{}, l0);
+    store_block(r + 32, IC<16 * DTL>{}, l1);
 #ifdef FA_STAMPS
     __builtin_amdgcn_s_waitcnt(0);
     const unsigned long long s_end = __builtin_amdgcn_s_memtime(), rt_end = __builtin_amdgcn_s_memrealtime();

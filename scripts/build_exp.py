@@ -1,0 +1,23 @@
+"""Build tagged stamps/experiment variants of the ABI library (only the instantiations that
+scripts/stamps.py c2 / c4 run). usage: python scripts/build_exp.py tag[:DEF1,DEF2][:flag flag] ..."""
+import sys
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+from flash_attention_cute_amd import _build  # noqa: E402
+
+ONLY = (("F16", 0, 128, 1), ("F16", 1, 128, 1))
+
+
+def one(spec):
+    parts = spec.split(":")
+    tag = parts[0]
+    defs = tuple(x for x in parts[1].split(",") if x) if len(parts) > 1 else ()
+    flags = tuple(parts[2].split()) if len(parts) > 2 else ()
+    return _build.build_abi(stamps=True, tag=tag, defines=defs, flags=flags, only=ONLY, force=True)
+
+
+with ThreadPoolExecutor(max_workers=4) as ex:
+    for r in ex.map(one, sys.argv[1:]):
+        print(r)

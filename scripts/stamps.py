@@ -19,7 +19,9 @@ sys.path.insert(0, str(ROOT))
 import bench  # noqa: E402
 
 cfg = bench.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "c2"]
-lib = ctypes.CDLL(str(ROOT / "build" / "stamps" / "libfa_gfx950.so"))
+import os  # noqa: E402
+
+lib = ctypes.CDLL(os.environ.get("FA_STAMPS_LIB", str(ROOT / "build" / "stamps" / "libfa_gfx950.so")))
 
 
 class P(ctypes.Structure):
