@@ -883,7 +883,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             const float m_new = Z.mE;
             const float seen = m_new > 0.5f * kNeg ? 1.f : 0.f;  // m_new * sc, or 0 before any visible key
             const float msc_new = Z.resc ? m_new * sc * seen : Z.msc;
-            Z.alpha = __builtin_amdgcn_exp2f(Z.msc - msc_new);
+            // a row's first visible key: O and l are still 0 and exp2(0 - m*sc) may overflow
+            Z.alpha = (Z.m <= 0.5f * kNeg) ? 0.f : __builtin_amdgcn_exp2f(Z.msc - msc_new);
             Z.m = m_new;
             Z.msc = msc_new;
             pin(Z.msc);
@@ -898,19 +899,6 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #else
         float x = kFold ? __builtin_amdgcn_exp2f(s[v]) : __builtin_amdgcn_exp2f(__builtin_fmaf(s[v], sc, -st[X].msc));
 #endif
-        pin(x);
-        s[v] = x;
-    };
-    // u_exp in two halves (the fma one MFMA gap ahead of the exp)
-    auto u_fma = [&](const int c, const int X, const int hf, const int v) {
-        f32x16 &s = S[c][2 * X + hf];
-        float x = __builtin_fmaf(s[v], sc, -st[X].msc);
-        pin(x);
-        s[v] = x;
-    };
-    auto u_ex2 = [&](const int c, const int X, const int hf, const int v) {
-        f32x16 &s = S[c][2 * X + hf];
-        float x = __builtin_amdgcn_exp2f(s[v]);
         pin(x);
         s[v] = x;
     };
@@ -975,22 +963,6 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                 else dma_one(vr, v_lds + (ks - NP) * 1024, vvo[ks - NP], ks == NP);
             }
             if constexpr (do_sm) {
-#if defined(FA_EXP_PREFMA)
-                // fma of the next gap's units one gap ahead: no fma -> exp dependency inside a gap
-                constexpr int UPG = 32 / G1;
-                static_for<32>([&](auto U) {
-                    constexpr int u = decltype(U)::value;
-                    if constexpr (g == 0 && u < UPG) u_fma(pr, u & 1, 1, u >> 1);
-                    if constexpr (u / UPG == g + 1) u_fma(pr, u & 1, 1, u >> 1);
-                });
-                static_for<32>([&](auto U) {
-                    constexpr int u = decltype(U)::value;
-                    if constexpr (u / UPG == g) {
-                        u_ex2(pr, u & 1, 1, u >> 1);
-                        if constexpr (u >= 2) u_fin(pr, u & 1, 1, (u >> 1) - 1);
-                    }
-                });
-#else
                 static_for<32>([&](auto U) {
                     constexpr int u = decltype(U)::value;
                     if constexpr ((u * G1) / 32 == g) {
@@ -998,7 +970,6 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                         if constexpr (u >= 2) u_fin(pr, u & 1, 1, (u >> 1) - 1);
                     }
                 });
-#endif
             }
             FA_SCHED_FENCE();
         });
