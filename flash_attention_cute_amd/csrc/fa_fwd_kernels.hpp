@@ -758,7 +758,6 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         n_pipe = min(n_pipe, x <= 0 ? 0 : x / kBlockN);
     }
     n_pipe = min(n_pipe, n_end);
-    if (dbg & 1) n_pipe = 0;  // debug: every tile through the non-pipelined body
 
     // ---- Q: this wave's 64 rows, B-operand fragments straight from HBM into AGPRs ----------
     // lane (h, r) of block X holds Q[mw + 32X + r][16*ks + 8*h + 0..7]; rows >= Sq read as 0
@@ -938,7 +937,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // tile of parity pr (32 units: block u&1, score u>>1 of half 1).
     constexpr int G1 = 4 * KS;
     auto phase1 = [&](const char *K, auto PAR, auto SM2, auto DMA, const rsrc_t &kr, const rsrc_t &vr,
-                      const uint32_t k_lds, const uint32_t v_lds) {
+                      const uint32_t k_lds, const uint32_t v_lds) __attribute__((always_inline)) {
         constexpr int c = decltype(PAR)::value, pr = c ^ 1;
         constexpr bool do_sm = decltype(SM2)::value, do_dma = decltype(DMA)::value;
         u32x4 kf[2][2];  // [buffer][key half]
@@ -979,7 +978,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         }
     };
     // the same second softmax half without MFMAs (drain and masked tiles)
-    auto sm2_all = [&](auto PAR) {
+    auto sm2_all = [&](auto PAR) __attribute__((always_inline)) {
         constexpr int c = decltype(PAR)::value;
         static_for<16>([&](auto VV) {
             constexpr int v = decltype(VV)::value;
@@ -1017,7 +1016,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         }
         return true;
     }(), "phase-2 softmax schedule");
-    auto phase2 = [&](const char *V, auto PPV, auto PSM, auto SM1) {
+    auto phase2 = [&](const char *V, auto PPV, auto PSM, auto SM1) __attribute__((always_inline)) {
         constexpr int cp = decltype(PPV)::value, cs = decltype(PSM)::value;
         constexpr bool do_sm = decltype(SM1)::value;
         u32x4 va[2][DTL];
@@ -1068,7 +1067,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         }
     };
     // the same first softmax half without MFMAs (masked tiles)
-    auto sm1_all = [&](auto PAR) {
+    auto sm1_all = [&](auto PAR) __attribute__((always_inline)) {
         constexpr int c = decltype(PAR)::value;
         static_for<2>([&](auto XX) {
             constexpr int X = decltype(XX)::value;
@@ -1123,7 +1122,17 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 
     // ---- pipelined tiles: iteration j = P1(S_j || softmax half 2 of j-1, DMA K_{j+1}, V_j),
     //      P2(O += P_{j-1} V_{j-1} || softmax half 1 of j), rescale, barrier -------------------
-    auto iter = [&](const int j, auto PAR) {
+    // causal diagonal / Sk tail: scores of keys past a row's last visible key -> kNeg
+    auto mask = [&](f32x16 &s0, f32x16 &s1, const int row, const int key0) __attribute__((always_inline)) {
+        const int lim = kCausal ? min(Sk - 1, row + diag) : Sk - 1;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int kk = key0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+            if (kk > lim) s0[i] = kNeg;
+            if (kk + 32 > lim) s1[i] = kNeg;
+        }
+    };
+    auto iter = [&](const int j, auto PAR, auto MASKED) __attribute__((always_inline)) {
         constexpr int c = decltype(PAR)::value, pr = c ^ 1;
         FA_STAMP(sa);
         const rsrc_t kr = make_rsrc(kp, tile_bytes((j + 1) * kBlockN, full_k, ks_));
@@ -1138,6 +1147,12 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #else
         phase1(lds + KV0 + c * T, PAR, IC<1>{}, IC<1>{}, kr, vr, lds_base + pr * T, lds_base + (2 + c) * T);
 #endif
+        if constexpr (decltype(MASKED)::value) {  // diagonal / tail tile: mask S before phase 2
+            s_ready(S[c][0], S[c][1]);
+            s_ready(S[c][2], S[c][3]);
+            mask(S[c][0], S[c][1], mw + r, j * kBlockN);
+            mask(S[c][2], S[c][3], mw + 32 + r, j * kBlockN);
+        }
         FA_STAMP(sb);
 #if defined(FA_EXP_NOSM)
         phase2(lds + KV0 + (2 + pr) * T, IC<pr>{}, PAR, IC<0>{});
@@ -1158,28 +1173,41 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         st_acc[4] += 1;
 #endif
     };
-    for (int j = 0; j < n_pipe; j += 2) {
-        iter(j, IC<0>{});
-        if (j + 1 < n_pipe) iter(j + 1, IC<1>{});
+    // every tile runs pipelined: first the tiles without a masked score, then (a second loop, so
+    // the hot loop carries no mask branch) the diagonal / tail tiles with a mask step between the
+    // phases. The debug variant (dbg & 1) runs all tiles through the plain body below instead.
+    const int n_loop = (dbg & 1) ? 0 : n_end;
+    const int n_unm = min(n_pipe, n_loop);
+    for (int j = 0; j < n_unm; j += 2) {
+        iter(j, IC<0>{}, IC<0>{});
+        if (j + 1 < n_unm) iter(j + 1, IC<1>{}, IC<0>{});
+    }
+    {
+        int j = n_unm;
+        if ((j & 1) && j < n_loop) iter(j++, IC<1>{}, IC<1>{});
+        for (; j < n_loop; j += 2) {
+            iter(j, IC<0>{}, IC<1>{});
+            if (j + 1 < n_loop) iter(j + 1, IC<1>{}, IC<1>{});
+        }
     }
     // drain the last pipelined tile: softmax half 2 and P.V
-    auto drain = [&](auto PAR) {
+    auto drain = [&](auto PAR) __attribute__((always_inline)) {
         constexpr int c = decltype(PAR)::value;
         sm2_all(PAR);
         phase2(lds + KV0 + (2 + c) * T, PAR, PAR, IC<0>{});
     };
-    if (n_pipe > 0) {
-        if ((n_pipe - 1) & 1) drain(IC<1>{}); else drain(IC<0>{});
+    if (n_loop > 0) {
+        if ((n_loop - 1) & 1) drain(IC<1>{}); else drain(IC<0>{});
     }
 
     FA_STAMP(s_pipe_end);
-    // ---- remaining tiles: masked, not pipelined --------------------------------------------
-    if (n_pipe < n_end) {
-        stage_v(n_pipe);  // the pipeline fetched V one tile late; catch up before the first one
+    // ---- debug variant: every tile masked, not pipelined -----------------------------------
+    if (n_loop < n_end) {
+        stage_v(n_loop);  // the pipeline fetched V one tile late; catch up before the first one
         dma_wait();
         __syncthreads();
     }
-    for (int j = n_pipe; j < n_end; ++j) {
+    for (int j = n_loop; j < n_end; ++j) {
         if (j + 1 < n_end) {
             stage_k(j + 1);
             stage_v(j + 1);
@@ -1190,17 +1218,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         phase1(K, IC<0>{}, IC<0>{}, IC<0>{}, k_rsrc(j), k_rsrc(j), 0u, 0u);
         s_ready(S[0][0], S[0][1]);
         s_ready(S[0][2], S[0][3]);
-        auto mask = [&](f32x16 &s0, f32x16 &s1, const int row) {
-            const int lim = kCausal ? min(Sk - 1, row + diag) : Sk - 1;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int kk = key0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                if (kk > lim) s0[i] = kNeg;
-                if (kk + 32 > lim) s1[i] = kNeg;
-            }
-        };
-        mask(S[0][0], S[0][1], mw + r);
-        mask(S[0][2], S[0][3], mw + 32 + r);
+        mask(S[0][0], S[0][1], mw + r, key0);
+        mask(S[0][2], S[0][3], mw + 32 + r, key0);
         sm1_all(IC<0>{});
         rescale();
         sm2_all(IC<0>{});

@@ -29,7 +29,7 @@ pytestmark = pytest.mark.gpu
 TOL = {torch.float16: (2e-3, 2e-3, 1e-4), torch.bfloat16: (1.6e-2, 1.6e-2, 1e-3)}
 
 
-@pytest.fixture(scope="module", params=["w4", "w8"])
+@pytest.fixture(scope="module", params=["w4", "w8", "w4slow"])
 def fa(device, request):
     # both kernel variants (include/fa_gfx950.h; FA_GFX950_VARIANT selects at launch time)
     import os
