@@ -36,6 +36,25 @@ unsigned long long *g_stamps = nullptr;
 
 unsigned long long *fa::stamp_buffer() { return g_stamps; }
 
+int64_t fa::w4_grid(int64_t nwg) {
+    // CU count per device, queried once (a racing first query writes the same value)
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = -1;
+    int n = dev >= 0 ? cus[dev] : 0;
+    if (n <= 0) {
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev < 0 ? 0 : dev) != hipSuccess || n <= 0)
+            n = 256;
+        if (dev >= 0) cus[dev] = n;
+    }
+    int64_t cap = n >= 8 ? n / 8 * 8 : n;
+    if (const char *e = getenv("FA_W4_GRID")) {
+        const long long v = atoll(e);
+        if (v > 0) cap = v;
+    }
+    return nwg < cap ? nwg : cap;
+}
+
 // Diagnostic hook (not in include/fa_gfx950.h): device buffer of 12 u64 per wave of the next
 // launches; honoured only by a -DFA_STAMPS=1 build of the kernels (scripts/stamps.py).
 extern "C" void fa_debug_set_stamps(void *device_buffer) { g_stamps = (unsigned long long *)device_buffer; }

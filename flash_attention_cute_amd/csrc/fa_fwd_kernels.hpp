@@ -589,6 +589,15 @@ __device__ __forceinline__ void agpr_qset(const u32x4 &v) {
     FA_CASE(160) FA_CASE(164) FA_CASE(168) FA_CASE(172) FA_CASE(176) FA_CASE(180) FA_CASE(184) FA_CASE(188)
 #undef FA_CASE
 }
+// asynchronous load of one Q fragment from rs + voff straight into a[QB .. QB+3]
+template <int QB>
+__device__ __forceinline__ void agpr_qload(const rsrc_t &rs, const int voff, const bool nop) {
+#define FA_CASE(N) \
+    if constexpr (QB == N) fa_agpr_qload_##N(rs, voff, nop);
+    FA_CASE(128) FA_CASE(132) FA_CASE(136) FA_CASE(140) FA_CASE(144) FA_CASE(148) FA_CASE(152) FA_CASE(156)
+    FA_CASE(160) FA_CASE(164) FA_CASE(168) FA_CASE(172) FA_CASE(176) FA_CASE(180) FA_CASE(184) FA_CASE(188)
+#undef FA_CASE
+}
 // first k-step with C = bias (the running reference max, kFoldScale)
 template <bool kF16, int QB>
 __device__ __forceinline__ void mfma_sq_bias(f32x16 &acc, const u32x4 &a, const f32x16 &bias) {
@@ -649,6 +658,19 @@ __device__ __forceinline__ void dma_one(const rsrc_t &rs, const uint32_t lds, co
     else
         asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "{m0}"(lds)
                      : "memory");
+}
+// the same to LDS address base + OFF: M0 is formed inside the asm (s_add_u32), so the kernel keeps
+// one LDS base in an SGPR instead of one materialised M0 value per (slot, piece)
+template <int OFF>
+__device__ __forceinline__ void dma_one_at(const rsrc_t &rs, const uint32_t base, const int voff, const bool nop) {
+    if (nop)
+        asm volatile("s_add_u32 m0, %2, %3\n\ts_nop 4\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
+                     "s"(base), "i"(OFF)
+                     : "memory", "m0", "scc");
+    else
+        asm volatile("s_add_u32 m0, %2, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
+                     "s"(base), "i"(OFF)
+                     : "memory", "m0", "scc");
 }
 // NP pieces from rs + voff[n] to LDS lds0 + n*1024
 template <int NP>
@@ -725,60 +747,83 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     const int r = lane & 31;
     const int h = lane >> 5;
 
-    // ---- XCD-aware work decode (as fa_fwd_w8) ------------------------------------------
-    const Work wk = decode_work<kCausal>(gridDim.x, blockIdx.x, n_qtiles, (int)p.num_heads_q);
-    const int hq = wk.hq, b = wk.b, qtile = wk.qtile;
-    const int hkv = hq / (int)p.head_q_per_group;
-
     const int Sq = (int)p.seqlen_q, Sk = (int)p.seqlen_kv, D = (int)p.headdim;
     const float sc = p.softmax_scale;
     const float thr_raw = kRescaleThr / sc;
-
-    const char *qb = (const char *)p.q_ptr + 2 * ((int64_t)b * p.q_batch_stride + (int64_t)hq * p.q_head_stride);
-    const char *kb = (const char *)p.k_ptr + 2 * ((int64_t)b * p.k_batch_stride + (int64_t)hkv * p.k_head_stride);
-    const char *vb = (const char *)p.v_ptr + 2 * ((int64_t)b * p.v_batch_stride + (int64_t)hkv * p.v_head_stride);
-    char *ob = (char *)p.o_ptr + 2 * ((int64_t)b * p.o_batch_stride + (int64_t)hq * p.o_head_stride);
-
-    const int m0 = qtile * kBlockM;
-    const int mw = m0 + wave * 64;  // block A: rows mw..mw+31, block B: rows mw+32..mw+63
     const int diag = Sk - Sq;
-
     const int n_blocks = (Sk + kBlockN - 1) / kBlockN;
-    int n_end = n_blocks;
-    if (kCausal) {
-        const int x = diag + min(m0 + kBlockM, Sq);
-        const int nb = x <= 0 ? 0 : (x + kBlockN - 1) / kBlockN;
-        n_end = min(nb, n_blocks);
-    }
-    // leading tiles with no masked score for any row of the WORKGROUP (pipelined; the same count
-    // for all waves keeps the LDS ring and the barriers aligned)
-    int n_pipe = Sk / kBlockN;
-    if (kCausal) {
-        const int x = m0 + diag + 1;  // keys visible to the workgroup's first row
-        n_pipe = min(n_pipe, x <= 0 ? 0 : x / kBlockN);
-    }
-    n_pipe = min(n_pipe, n_end);
+
+    // ---- persistent schedule ----------------------------------------------------------------
+    // The grid holds about one workgroup per CU; each walks Q blocks (q-tile, q-head, batch) of its
+    // own XCD's range of the XCD-aware logical order (decode_work), one round per gx workgroups of
+    // the XCD, snake-ordered (odd rounds reversed) so that a heavy-first causal order balances
+    // without a work queue. The next block's Q fragments and first K tile are fetched while the
+    // current block drains its pipeline and stores O.
+    const uint32_t nwg = (uint32_t)n_qtiles * (uint32_t)p.num_heads_q * (uint32_t)p.batch_size;
+    const uint32_t xcd = blockIdx.x & 7, cx = blockIdx.x >> 3;
+    const uint32_t gx = (gridDim.x - xcd + 7) >> 3;  // workgroups of this XCD
+    const uint32_t cnt = (nwg - xcd + 7) >> 3;       // Q blocks of this XCD
+    auto block_of = [&](const uint32_t rnd) { return rnd * gx + ((rnd & 1) ? gx - 1 - cx : cx); };
+    uint32_t rnd = 0, kblk = block_of(0);
+    if (kblk >= cnt) return;
+
+    // per-block geometry (set_block)
+    const char *qb, *kb, *vb;
+    char *ob;
+    int m0, mw, n_end, n_pipe;
+    auto set_block = [&](const uint32_t k) {
+        const Work wk = decode_work<kCausal>(nwg, xcd + 8 * k, n_qtiles, (int)p.num_heads_q);
+        const int hq = wk.hq, b = wk.b;
+        const int hkv = hq / (int)p.head_q_per_group;
+        qb = (const char *)p.q_ptr + 2 * ((int64_t)b * p.q_batch_stride + (int64_t)hq * p.q_head_stride);
+        kb = (const char *)p.k_ptr + 2 * ((int64_t)b * p.k_batch_stride + (int64_t)hkv * p.k_head_stride);
+        vb = (const char *)p.v_ptr + 2 * ((int64_t)b * p.v_batch_stride + (int64_t)hkv * p.v_head_stride);
+        ob = (char *)p.o_ptr + 2 * ((int64_t)b * p.o_batch_stride + (int64_t)hq * p.o_head_stride);
+        m0 = wk.qtile * kBlockM;
+        mw = m0 + wave * 64;  // block A: rows mw..mw+31, block B: rows mw+32..mw+63
+        n_end = n_blocks;
+        if (kCausal) {
+            const int x = diag + min(m0 + kBlockM, Sq);
+            const int nb = x <= 0 ? 0 : (x + kBlockN - 1) / kBlockN;
+            n_end = min(nb, n_blocks);
+        }
+        // leading tiles with no masked score for any row of the WORKGROUP (pipelined; the same
+        // count for all waves keeps the LDS ring and the barriers aligned)
+        n_pipe = Sk / kBlockN;
+        if (kCausal) {
+            const int x = m0 + diag + 1;  // keys visible to the workgroup's first row
+            n_pipe = min(n_pipe, x <= 0 ? 0 : x / kBlockN);
+        }
+        n_pipe = min(n_pipe, n_end);
+    };
+    set_block(kblk);
 
     // ---- Q: this wave's 64 rows, B-operand fragments straight from HBM into AGPRs ----------
-    // lane (h, r) of block X holds Q[mw + 32X + r][16*ks + 8*h + 0..7]; rows >= Sq read as 0
-    {
+    // lane (h, r) of block X holds Q[mw + 32X + r][16*ks + 8*h + 0..7]; rows >= Sq read as 0.
+    // Asynchronous: retired by the vmcnt wait ahead of the block's first barrier.
+    auto load_q = [&]() __attribute__((always_inline)) {
         const int qs = (int)p.q_seqlen_stride;
         const rsrc_t qr = make_rsrc(qb + 2 * (int64_t)mw * qs, slab_bytes(min(Sq - mw, 64), qs, D));
-        u32x4 qv[2 * KS];
-#pragma unroll
-        for (int X = 0; X < 2; ++X)
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                const bool ok = kExactD || 16 * ks + 8 * h < D;  // columns past D read as 0
-                qv[X * KS + ks] = __builtin_amdgcn_raw_buffer_load_b128(
-                    qr, ok ? (32 * X + r) * qs * 2 + 32 * ks + 16 * h : 0x7ffffff0, 0, 0);
-            }
+        auto qoff = [&](const int X, const int ks) {
+            const bool ok = kExactD || 16 * ks + 8 * h < D;  // columns past D read as 0
+            return ok ? (32 * X + r) * qs * 2 + 32 * ks + 16 * h : 0x7ffffff0;
+        };
         if constexpr (kFold) {
+            u32x4 qv[2 * KS];
 #pragma unroll
-            for (int i = 0; i < 2 * KS; ++i) qv[i] = DT::scale8(qv[i], sc);
+            for (int X = 0; X < 2; ++X)
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks)
+                    qv[X * KS + ks] = DT::scale8(__builtin_amdgcn_raw_buffer_load_b128(qr, qoff(X, ks), 0, 0), sc);
+            static_for<2 * KS>([&](auto I) { agpr_qset<QB + 4 * decltype(I)::value>(qv[decltype(I)::value]); });
+        } else {
+            static_for<2 * KS>([&](auto I) {
+                constexpr int i = decltype(I)::value;
+                agpr_qload<QB + 4 * i>(qr, qoff(i / KS, i % KS), i == 0);
+            });
         }
-        static_for<2 * KS>([&](auto I) { agpr_qset<QB + 4 * decltype(I)::value>(qv[decltype(I)::value]); });
-    }
+    };
+    load_q();
 
     // ---- LDS-DMA staging: this wave writes pieces (wave*NP + n) of each K and V tile --------
     const int ks_ = (int)p.k_seqlen_stride, vs_ = (int)p.v_seqlen_stride;
@@ -824,17 +869,11 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         bool resc, seen, vis; // kFold: the row has seen a visible key; this tile has one
     };
     Sm st[2];
-#pragma unroll
-    for (int X = 0; X < 2; ++X) st[X] = {kNeg, 0.f, 1.f, kNeg, kNeg, 0.f, 0.f, 0.f, false, false, false};
     f32x16 bias[2];  // kFold: -m*s' per lane, the C operand of the first S k-step
-#pragma unroll
-    for (int X = 0; X < 2; ++X) bias[X] = (f32x16){};
     const uint32_t one2 = F ? 0x3C003C00u : 0x3F803F80u;
     const u32x4 ones = {one2, one2, one2, one2};  // kLsum: A operand of the row-sum MFMA
-    if constexpr (kLsum) fa_agpr_zero_l();
     f32x16 S[2][4];  // [tile parity][2 * block + half]: half 0 = keys 0-31, 1 = keys 32-63
     u32x4 P[2][8];   // [tile parity][4 * block + k-step]
-    if constexpr (DTL == 4) fa_agpr_zero_4(); else fa_agpr_zero_2();
 
     // ---- softmax units (each a few VALU instructions, placed between single MFMAs) ----------
     // max chain unit i (0..15) of block X: scores i of both halves
@@ -931,13 +970,14 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         }
     };
 
+    const uint32_t lds_base = lds_u32(lds) + wave * NP * 1024;  // this wave's pieces of slot 0
     // ---- phase 1: S[c] = K.Q^T for both blocks (4*KS single MFMAs) ----------------------------
     // gap g (after MFMA g): next k-step's K fragments (gaps 4ks, 4ks+1; Q is in AGPRs), one LDS-DMA piece
     // (gap 4ks+2: K_{j+1} pieces, then V_j pieces), and with SM2 the second softmax half of the
     // tile of parity pr (32 units: block u&1, score u>>1 of half 1).
     constexpr int G1 = 4 * KS;
-    auto phase1 = [&](const char *K, auto PAR, auto SM2, auto DMA, const rsrc_t &kr, const rsrc_t &vr,
-                      const uint32_t k_lds, const uint32_t v_lds) __attribute__((always_inline)) {
+    auto phase1 = [&](const char *K, auto PAR, auto SM2, auto DMA, const rsrc_t &kr, const rsrc_t &vr)
+        __attribute__((always_inline)) {
         constexpr int c = decltype(PAR)::value, pr = c ^ 1;
         constexpr bool do_sm = decltype(SM2)::value, do_dma = decltype(DMA)::value;
         u32x4 kf[2][2];  // [buffer][key half]
@@ -958,8 +998,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                 kf[cb ^ 1][1] = *(const u32x4 *)(K + 32 * RB + k_addr[ks + 1]);
             }
             if constexpr (do_dma && i == 2) {
-                if constexpr (ks < NP) dma_one(kr, k_lds + ks * 1024, kvo[ks], ks == 0);
-                else dma_one(vr, v_lds + (ks - NP) * 1024, vvo[ks - NP], ks == NP);
+                if constexpr (ks < NP) dma_one_at<pr * T + ks * 1024>(kr, lds_base, kvo[ks], ks == 0);
+                else dma_one_at<(2 + c) * T + (ks - NP) * 1024>(vr, lds_base, vvo[ks - NP], ks == NP);
             }
             if constexpr (do_sm) {
                 static_for<32>([&](auto U) {
@@ -1093,17 +1133,32 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // full_k / full_v bytes, the Sk tail tile fewer, a tile past Sk none
     const uint32_t full_k = slab_bytes(kBlockN, ks_, D), full_v = slab_bytes(kBlockN, vs_, D);
     const int64_t step_k = 2 * (int64_t)kBlockN * ks_, step_v = 2 * (int64_t)kBlockN * vs_;
-    const char *kp = kb + step_k;  // K tile j + 1 of iteration j
-    const char *vp = vb;           // V tile j of iteration j
+    const char *kp, *vp;  // K tile j + 1 / V tile j of iteration j
     auto tile_bytes = [&](const int key0, const uint32_t full, const int stride) {
         const int rows = Sk - key0;
         return rows >= kBlockN ? full : slab_bytes(rows, stride, D);
     };
-    const uint32_t lds_base = lds_u32(lds) + wave * NP * 1024;  // this wave's pieces of slot 0
 
-    // ---- prologue -------------------------------------------------------------------------
+    stage_k(0);  // the first block's K_0 (its Q is in flight above)
+    for (;;) {
+    // ---- block prologue: Q and K_0 of this block are in flight ------------------------------
+#ifdef FA_STAMPS
+    st_t0 = __builtin_amdgcn_s_memtime();
+    st_rt0 = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st_acc[i] = 0;
+#endif
+    kp = kb + step_k;
+    vp = vb;
+#pragma unroll
+    for (int X = 0; X < 2; ++X) {
+        st[X] = {kNeg, 0.f, 1.f, kNeg, kNeg, 0.f, 0.f, 0.f, false, false, false};
+        bias[X] = (f32x16){};
+    }
+    if constexpr (kLsum) fa_agpr_zero_l();
+    if constexpr (DTL == 4) fa_agpr_zero_4(); else fa_agpr_zero_2();
     // tile -1 of the pipeline is empty: its S = kNeg gives P = 0, and its P.V reads V slot 1,
-    // zeroed here so that 0 * V stays 0.
+    // zeroed here so that 0 * V stays 0 (the previous block's V may hold non-finite values).
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         S[1][1][i] = kNeg;
@@ -1111,13 +1166,13 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) P[1][i] = (u32x4){0, 0, 0, 0};
+    __syncthreads();  // every wave is past the previous block's reads of V slot 1
     {
         constexpr int per_thread = T / 256 / 16;
 #pragma unroll
         for (int i = 0; i < per_thread; ++i) *(u32x4 *)(lds + KV0 + 3 * T + (i * 256 + tid) * 16) = (u32x4){0, 0, 0, 0};
     }
-    if (n_end > 0) stage_k(0);
-    dma_wait();       // K_0 landed
+    dma_wait();       // Q, K_0 landed (and the previous block's O stores retired)
     __syncthreads();  // visible to every wave
 
     // ---- pipelined tiles: iteration j = P1(S_j || softmax half 2 of j-1, DMA K_{j+1}, V_j),
@@ -1141,11 +1196,11 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         vp += step_v;
         // FA_EXP_*: timing experiments of the stamps build only (results are garbage)
 #if defined(FA_EXP_NOSM)
-        phase1(lds + KV0 + c * T, PAR, IC<0>{}, IC<1>{}, kr, vr, lds_base + pr * T, lds_base + (2 + c) * T);
+        phase1(lds + KV0 + c * T, PAR, IC<0>{}, IC<1>{}, kr, vr);
 #elif defined(FA_EXP_NODMA)
-        phase1(lds + KV0 + c * T, PAR, IC<1>{}, IC<0>{}, kr, vr, lds_base + pr * T, lds_base + (2 + c) * T);
+        phase1(lds + KV0 + c * T, PAR, IC<1>{}, IC<0>{}, kr, vr);
 #else
-        phase1(lds + KV0 + c * T, PAR, IC<1>{}, IC<1>{}, kr, vr, lds_base + pr * T, lds_base + (2 + c) * T);
+        phase1(lds + KV0 + c * T, PAR, IC<1>{}, IC<1>{}, kr, vr);
 #endif
         if constexpr (decltype(MASKED)::value) {  // diagonal / tail tile: mask S before phase 2
             s_ready(S[c][0], S[c][1]);
@@ -1190,17 +1245,6 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             if (j + 1 < n_loop) iter(j + 1, IC<1>{}, IC<1>{});
         }
     }
-    // drain the last pipelined tile: softmax half 2 and P.V
-    auto drain = [&](auto PAR) __attribute__((always_inline)) {
-        constexpr int c = decltype(PAR)::value;
-        sm2_all(PAR);
-        phase2(lds + KV0 + (2 + c) * T, PAR, PAR, IC<0>{});
-    };
-    if (n_loop > 0) {
-        if ((n_loop - 1) & 1) drain(IC<1>{}); else drain(IC<0>{});
-    }
-
-    FA_STAMP(s_pipe_end);
     // ---- debug variant: every tile masked, not pipelined -----------------------------------
     if (n_loop < n_end) {
         stage_v(n_loop);  // the pipeline fetched V one tile late; catch up before the first one
@@ -1215,7 +1259,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         const char *K = lds + KV0 + (j & 1) * T;
         const char *V = lds + KV0 + (2 + (j & 1)) * T;
         const int key0 = j * kBlockN;
-        phase1(K, IC<0>{}, IC<0>{}, IC<0>{}, k_rsrc(j), k_rsrc(j), 0u, 0u);
+        phase1(K, IC<0>{}, IC<0>{}, IC<0>{}, k_rsrc(j), k_rsrc(j));
         s_ready(S[0][0], S[0][1]);
         s_ready(S[0][2], S[0][3]);
         mask(S[0][0], S[0][1], mw + r, key0);
@@ -1228,10 +1272,36 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         __syncthreads();
     }
 
+    // ---- next block: its Q fragments and K_0 go in flight under this block's drain and stores.
+    // Every wave is past this block's last barrier: the Q AGPRs and both K slots are free (the
+    // drain reads only a V slot).
+    char *const ob_c = ob;
+    const int mw_c = mw;
+#ifdef FA_STAMPS
+    const uint32_t blk_c = xcd + 8 * kblk;
+#endif
+    kblk = block_of(++rnd);
+    const bool more = kblk < cnt;
+    if (more) {
+        set_block(kblk);
+        load_q();
+        stage_k(0);
+    }
+    // drain the last pipelined tile: softmax half 2 and P.V
+    auto drain = [&](auto PAR) __attribute__((always_inline)) {
+        constexpr int c = decltype(PAR)::value;
+        sm2_all(PAR);
+        phase2(lds + KV0 + (2 + c) * T, PAR, PAR, IC<0>{});
+    };
+    if (n_loop > 0) {
+        if ((n_loop - 1) & 1) drain(IC<1>{}); else drain(IC<0>{});
+    }
+    FA_STAMP(s_pipe_end);
+
     // ---- epilogue ---------------------------------------------------------------------------
     mfma_drain();  // last asm MFMA -> AGPR reads
     const int os_ = (int)p.o_seqlen_stride;
-    const rsrc_t orr = make_rsrc(ob + 2 * (int64_t)mw * os_, slab_bytes(min(Sq - mw, 64), os_, D));
+    const rsrc_t orr = make_rsrc(ob_c + 2 * (int64_t)mw_c * os_, slab_bytes(min(Sq - mw_c, 64), os_, D));
     auto store_block = [&](const int row, auto OBASE, const float l_tot) {
         constexpr int ob0 = decltype(OBASE)::value;
         f32x16 o[DTL];
@@ -1267,22 +1337,26 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     store_block(r, IC<0>{}, l0);
     store_block(r + 32, IC<16 * DTL>{}, l1);
 #ifdef FA_STAMPS
-    __builtin_amdgcn_s_waitcnt(0);
-    const unsigned long long s_end = __builtin_amdgcn_s_memtime(), rt_end = __builtin_amdgcn_s_memrealtime();
-    if (stamps && lane == 0) {
-        // [total, p1, p2+rescale, dma wait, barrier, tiles, pipelined-loop span, masked tiles,
-        //  epilogue, realtime (100 MHz ticks), start time]
-        unsigned long long *o = stamps + ((size_t)blockIdx.x * 4 + wave) * 12;
-        o[0] = s_end - st_t0;
-        for (int i = 0; i < 5; ++i) o[1 + i] = st_acc[i];
-        o[6] = s_pipe_end - st_t0;
-        o[7] = s_masked_end - s_pipe_end;
-        o[8] = s_end - s_masked_end;
-        o[9] = rt_end - st_rt0;
-        o[10] = st_t0;
-        o[11] = xcc_id();
+    {
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long s_end = __builtin_amdgcn_s_memtime(), rt_end = __builtin_amdgcn_s_memrealtime();
+        if (stamps && lane == 0) {
+            // per Q block: [total, p1, p2+rescale, dma wait, barrier, tiles, pipelined-loop span,
+            //  (unused), epilogue, realtime (100 MHz ticks), start time, xcc]
+            unsigned long long *o = stamps + ((size_t)blk_c * 4 + wave) * 12;
+            o[0] = s_end - st_t0;
+            for (int i = 0; i < 5; ++i) o[1 + i] = st_acc[i];
+            o[6] = s_pipe_end - st_t0;
+            o[7] = s_masked_end - s_pipe_end;
+            o[8] = s_end - s_masked_end;
+            o[9] = rt_end - st_rt0;
+            o[10] = st_t0;
+            o[11] = xcc_id();
+        }
     }
 #endif
+    if (!more) break;
+    }  // persistent block loop
 }
 #undef FA_STAMP
 
@@ -1296,7 +1370,8 @@ int launch_one(const fa_fwd_params &p, hipStream_t stream) {
         hipLaunchKernelGGL((fa_fwd_w8<DT, C, kD, kExact>), dim3((uint32_t)nwg), dim3(kThreads), 0, stream, p,
                            (int)n_qtiles);
     else
-        hipLaunchKernelGGL((fa_fwd_w4<DT, C, kD, kExact>), dim3((uint32_t)nwg), dim3(256), 0, stream, p,
+        // persistent: about one workgroup per CU (the kernel walks the Q blocks itself)
+        hipLaunchKernelGGL((fa_fwd_w4<DT, C, kD, kExact>), dim3((uint32_t)w4_grid(nwg)), dim3(256), 0, stream, p,
                            (int)n_qtiles, variant == 2 ? 1 : 0, stamp_buffer());
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "HIP launch failed: %s", hipGetErrorString(e));

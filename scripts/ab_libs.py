@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of several builds of the C-ABI library on one bench config (same process,
+same device, same inputs), so device-to-device clock differences cancel out.
+usage: python scripts/ab_libs.py <cfg> <lib.so> [<lib.so> ...]   (env AB_REPS, AB_ITERS)
+"""
+import ctypes
+import os
+import sys
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+import bench  # noqa: E402
+
+cfg = bench.CONFIGS[sys.argv[1]]
+libs = [ctypes.CDLL(os.path.abspath(p)) for p in sys.argv[2:]]
+
+
+class P(ctypes.Structure):
+    _fields_ = ([(n, ctypes.c_void_p) for n in ("q", "k", "v", "o")]
+                + [(n, ctypes.c_int64) for n in ("B", "Hq", "Hkv", "Sq", "Sk", "D", "g")]
+                + [(f"s{i}", ctypes.c_int64) for i in range(12)] + [("scale", ctypes.c_float)])
+
+
+dev = torch.device("cuda:0")
+dt = torch.float16 if cfg["dtype"] == "fp16" else torch.bfloat16
+torch.manual_seed(0)
+q = torch.randn(cfg["B"], cfg["Hq"], cfg["Sq"], cfg["D"], device=dev, dtype=dt)
+k = torch.randn(cfg["B"], cfg["Hkv"], cfg["Sk"], cfg["D"], device=dev, dtype=dt)
+v = torch.randn_like(k)
+outs = [torch.empty_like(q) for _ in libs]
+stream = torch.cuda.current_stream().cuda_stream
+
+
+def params(o):
+    st = (q, k, v, o)
+    return P(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), cfg["B"], cfg["Hq"], cfg["Hkv"], cfg["Sq"],
+             cfg["Sk"], cfg["D"], cfg["Hq"] // cfg["Hkv"], *[t.stride(0) for t in st], *[t.stride(1) for t in st],
+             *[t.stride(2) for t in st], cfg["D"] ** -0.5 * 1.4426950408889634)
+
+
+ps = [params(o) for o in outs]
+dcode = 0 if dt == torch.float16 else 1
+
+
+def run(i, n):
+    for _ in range(n):
+        assert libs[i].fa_fwd_gfx950(ctypes.byref(ps[i]), dcode, int(cfg["causal"]), ctypes.c_void_p(stream)) == 0
+
+
+flops = 4.0 * cfg["B"] * cfg["Hq"] * cfg["Sq"] * cfg["Sk"] * cfg["D"] * (0.5 if cfg["causal"] else 1.0)
+iters = int(os.environ.get("AB_ITERS", "30"))
+for i in range(len(libs)):
+    run(i, 10)
+torch.cuda.synchronize()
+res = [[] for _ in libs]
+for rep in range(int(os.environ.get("AB_REPS", "5"))):
+    for i in range(len(libs)):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        run(i, iters)
+        b.record()
+        torch.cuda.synchronize()
+        res[i].append(flops * iters / (a.elapsed_time(b) * 1e-3) / 1e12)
+for i, p in enumerate(sys.argv[2:]):
+    r = sorted(res[i])
+    d = (outs[i].float() - outs[0].float()).abs().max().item()
+    print(f"{sys.argv[1]} {p}: median {r[len(r) // 2]:.1f} TFLOPS  (min {r[0]:.1f} max {r[-1]:.1f})  max|o-o0| {d:.2e}")
