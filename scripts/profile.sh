@@ -12,6 +12,8 @@ cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $BENCH > $OUT/trace.log 2>&1 || { tail -20 $OUT/trace.log; exit 1; }
 for CTR in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" ; do
   N=$(echo $CTR | tr ' ' '_')
-  timeout -k 10 300 rocprofv3 --pmc $CTR --output-format csv -d $OUT/pmc_$N -o run -- python3 $BENCH > $OUT/pmc_$N.log 2>&1 || { echo "pmc $CTR failed"; tail -5 $OUT/pmc_$N.log; }
+  timeout -k 10 300 rocprofv3 --pmc $CTR --output-format csv -d $OUT/pmc_$N -o run -- python3 $BENCH --warmup-seconds 0.5 > $OUT/pmc_$N.log 2>&1 || { echo "pmc $CTR failed"; tail -5 $OUT/pmc_$N.log; }
 done
+cp $OUT/trace/*/run_kernel_stats.csv $OUT/kernel_stats.csv 2>/dev/null || find $OUT/trace -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
+grep "^{\"metric\"" $OUT/trace.log > $OUT/bench_line.json
 find $OUT -name "*.csv" | head -50
