@@ -679,6 +679,9 @@ __device__ __forceinline__ void dma_pieces(const rsrc_t &rs, const uint32_t lds0
     for (int n = 0; n < NP; ++n) dma_one(rs, lds0 + n * 1024, voff[n], n == 0);
 }
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// s_waitcnt immediate for vmcnt(n) alone (gfx9 encoding: vmcnt[3:0] + vmcnt[5:4] at [15:14], expcnt
+// 7, lgkmcnt 15)
+constexpr int vmcnt_enc(int n) { return (n & 15) | (((n >> 4) & 3) << 14) | 0x70 | 0xF00; }
 
 // =============================================================================================
 // fa_fwd_w4: one wave per SIMD, 64 query rows per wave (two 32-row blocks A and B). Per KV tile j:
@@ -735,6 +738,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     constexpr int T = G::kTileBytes;
     constexpr int NP = T / 4 / 1024;  // LDS-DMA pieces per wave per K or V tile (4 / 2)
     constexpr int ROWS_PER_PIECE = 1024 / RB;
+    constexpr int kOStores = 2 * DTL * 2;  // O stores per wave and block (epilogue)
     constexpr int QB = 128;  // Q fragments: AGPRs a[QB + 4*(X*KS + ks)] (fa_agpr_asm.inc)
     // LDS: K slots 0,1 | V slots 0,1 (64 KiB at D = 128), so every fragment read is a per-lane base
     // plus a 16-bit immediate offset. Q is read once from HBM straight into AGPRs.
@@ -1172,8 +1176,11 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #pragma unroll
         for (int i = 0; i < per_thread; ++i) *(u32x4 *)(lds + KV0 + 3 * T + (i * 256 + tid) * 16) = (u32x4){0, 0, 0, 0};
     }
-    dma_wait();       // Q, K_0 landed (and the previous block's O stores retired)
+    // Q, K_0 landed. After the first block the previous block's O stores were issued after these
+    // loads: leave them in flight (vmcnt counts stores too, in issue order)
+    if (rnd == 0) dma_wait(); else __builtin_amdgcn_s_waitcnt(vmcnt_enc(kOStores));
     __syncthreads();  // visible to every wave
+    FA_STAMP(s_pro);
 
     // ---- pipelined tiles: iteration j = P1(S_j || softmax half 2 of j-1, DMA K_{j+1}, V_j),
     //      P2(O += P_{j-1} V_{j-1} || softmax half 1 of j), rescale, barrier -------------------
@@ -1245,6 +1252,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             if (j + 1 < n_loop) iter(j + 1, IC<1>{}, IC<1>{});
         }
     }
+    FA_STAMP(s_loop_end);
     // ---- debug variant: every tile masked, not pipelined -----------------------------------
     if (n_loop < n_end) {
         stage_v(n_loop);  // the pipeline fetched V one tile late; catch up before the first one
@@ -1324,9 +1332,10 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                 const auto x0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
                 const auto x1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
                 const int d0 = dt * 32 + 8 * (gp + h);
-                if (kExactD || d0 < D)
-                    __builtin_amdgcn_raw_buffer_store_b128((u32x4){x0[0], x1[0], x0[1], x1[1]}, orr, orow + 2 * d0, 0,
-                                                           0);
+                // unconditional (columns past D go out of range and are dropped): every wave issues
+                // exactly kOStores stores per block, which the next block's counted wait relies on
+                __builtin_amdgcn_raw_buffer_store_b128((u32x4){x0[0], x1[0], x0[1], x1[1]}, orr,
+                                                       (kExactD || d0 < D) ? orow + 2 * d0 : 0x7ffffff0, 0, 0);
             }
         }
     };
@@ -1341,13 +1350,13 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         __builtin_amdgcn_s_waitcnt(0);
         const unsigned long long s_end = __builtin_amdgcn_s_memtime(), rt_end = __builtin_amdgcn_s_memrealtime();
         if (stamps && lane == 0) {
-            // per Q block: [total, p1, p2+rescale, dma wait, barrier, tiles, pipelined-loop span,
-            //  (unused), epilogue, realtime (100 MHz ticks), start time, xcc]
+            // per Q block: [total, p1, p2+rescale, dma wait, barrier, tiles, drain (+ next block's
+            //  prefetch issue), prologue, epilogue, realtime (100 MHz ticks), start time, xcc]
             unsigned long long *o = stamps + ((size_t)blk_c * 4 + wave) * 12;
             o[0] = s_end - st_t0;
             for (int i = 0; i < 5; ++i) o[1 + i] = st_acc[i];
-            o[6] = s_pipe_end - st_t0;
-            o[7] = s_masked_end - s_pipe_end;
+            o[6] = s_pipe_end - s_loop_end;
+            o[7] = s_pro - st_t0;
             o[8] = s_end - s_masked_end;
             o[9] = rt_end - st_rt0;
             o[10] = st_t0;

@@ -64,7 +64,7 @@ assert lib.fa_fwd_gfx950(ctypes.byref(p), 0 if dt == torch.float16 else 1, int(c
 torch.cuda.synchronize()
 lib.fa_debug_set_stamps(ctypes.c_void_p(0))
 s = buf.view(-1, 12).cpu().double()
-names = ["total", "p1", "p2+resc", "dma_wait", "barrier", "tiles", "pipe_span", "masked", "epilogue", "realtime"]
+names = ["total", "p1", "p2+resc", "dma_wait", "barrier", "tiles", "drain", "prologue", "epilogue", "realtime"]
 med = s.median(dim=0).values
 print(f"{cfg['workload']}: {n} warm launches, {s.shape[0]} waves")
 for i, nm in enumerate(names):
@@ -77,3 +77,6 @@ print(f"  in-kernel clock median {float(clk.median()):.3f} GHz")
 start = s[:, 10] - s[:, 10].min()
 print(f"  launch span {float((s[:, 10] + s[:, 0]).max() - s[:, 10].min()):.0f} cycles, start spread "
       f"{float(start.max()):.0f}")
+for i, nm in [(6, "drain"), (7, "prologue"), (8, "epilogue")]:
+    qs = torch.quantile(s[:, i], torch.tensor([0.1, 0.5, 0.9, 0.99], dtype=torch.float64))
+    print(f"  {nm:10s} p10 {qs[0]:8.0f}  p50 {qs[1]:8.0f}  p90 {qs[2]:8.0f}  p99 {qs[3]:8.0f}")
