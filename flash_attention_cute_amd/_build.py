@@ -83,15 +83,17 @@ def build_abi(force: bool = False, verbose: bool = False, stamps: bool = False, 
     from concurrent.futures import ThreadPoolExecutor
 
     # diagnostic builds (stamps, experiments) go to build/stamps[_<tag>]/, never over the product
-    sdir = "stamps" + (f"_{tag}" if tag else "")
-    out_lib = ROOT / "build" / sdir / "libfa_gfx950.so" if stamps else ABI_LIB
+    # (experiment builds without stamps: tag + defines, to build/exp_<tag>/, for scripts/ab_libs.py)
+    sdir = ("stamps" if stamps else "exp") + (f"_{tag}" if tag else "")
+    diag = stamps or bool(tag)
+    out_lib = ROOT / "build" / sdir / "libfa_gfx950.so" if diag else ABI_LIB
     out_lib.parent.mkdir(parents=True, exist_ok=True)
     if not force and not _stale(out_lib, abi_sources()):
         return out_lib
     if not HIPCC.exists():
         raise RuntimeError(f"hipcc not found at {HIPCC}")
-    objdir = ROOT / "build" / (f"obj_{sdir}" if stamps else "obj")
-    extra = (["-DFA_STAMPS=1"] + [f"-D{d}" for d in defines] + list(flags)) if stamps else []
+    objdir = ROOT / "build" / (f"obj_{sdir}" if diag else "obj")
+    extra = ((["-DFA_STAMPS=1"] if stamps else []) + [f"-D{d}" for d in defines] + list(flags)) if diag else []
     objdir.mkdir(parents=True, exist_ok=True)
     cmds = []
     objs = []

@@ -635,9 +635,15 @@ constexpr int kLgkm0 = 0xC07F;
 
 // Opaque redefinition: ties a value to this point of the (volatile-asm ordered) instruction stream,
 // so IR-level sinking / hoisting cannot move the VALU slices out of their MFMA gap.
+#ifndef FA_NOPIN
 __device__ __forceinline__ void pin(float &x) { asm volatile("" : "+v"(x)); }
 __device__ __forceinline__ void pin(u32x4 &x) { asm volatile("" : "+v"(x)); }
 __device__ __forceinline__ void pin(uint32_t &x) { asm volatile("" : "+v"(x)); }
+#else
+__device__ __forceinline__ void pin(float &) {}
+__device__ __forceinline__ void pin(u32x4 &) {}
+__device__ __forceinline__ void pin(uint32_t &) {}
+#endif
 
 __device__ __forceinline__ uint32_t lds_u32(const void *ptr) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)ptr;
@@ -739,6 +745,13 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     constexpr int NP = T / 4 / 1024;  // LDS-DMA pieces per wave per K or V tile (4 / 2)
     constexpr int ROWS_PER_PIECE = 1024 / RB;
     constexpr int kOStores = 2 * DTL * 2;  // O stores per wave and block (epilogue)
+#ifdef FA_V0
+    constexpr int kV0 = FA_V0;
+#else
+    constexpr int kV0 = 16;  // early scores per block and tile (phase 2); the rest run in phase 1
+#endif
+    static_assert(kV0 >= 4 && kV0 < 32 && kV0 % 2 == 0, "kV0");
+    constexpr int kNL = 2 * (32 - kV0);  // late exp units of phase 1
     constexpr int QB = 128;  // Q fragments: AGPRs a[QB + 4*(X*KS + ks)] (fa_agpr_asm.inc)
     // LDS: K slots 0,1 | V slots 0,1 (64 KiB at D = 128), so every fragment read is a per-lane base
     // plus a 16-bit immediate offset. Q is read once from HBM straight into AGPRs.
@@ -949,7 +962,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     auto u_fin = [&](const int c, const int X, const int hf, const int v) {
         const f32x16 &s = S[c][2 * X + hf];
         if constexpr (!kLsum) {
-            float &acc = hf ? st[X].l : st[X].t;
+            // half 1 and the late scores of half 0 (run after the tile's rescale) add into l
+            float &acc = (16 * hf + v >= kV0) ? st[X].l : st[X].t;
             acc = (hf == 0 && v == 0) ? s[0] : acc + s[v];
             pin(acc);
         }
@@ -975,6 +989,13 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     };
 
     const uint32_t lds_base = lds_u32(lds) + wave * NP * 1024;  // this wave's pieces of slot 0
+    // ---- softmax split: of each block's 32 scores of a tile (index q = 16 * half + v), q < kV0 are
+    // exponentiated in phase 2 right after the tile's rescale decision ("early", summed into t), the
+    // rest in the next phase 1 ("late", summed into l).
+    struct Late {  // late unit u: block u & 1, score index q = kV0 + u / 2 (q = 16 * half + v)
+        static constexpr int hf(int u) { return (kV0 + (u >> 1)) >> 4; }
+        static constexpr int v(int u) { return (kV0 + (u >> 1)) & 15; }
+    };
     // ---- phase 1: S[c] = K.Q^T for both blocks (4*KS single MFMAs) ----------------------------
     // gap g (after MFMA g): next k-step's K fragments (gaps 4ks, 4ks+1; Q is in AGPRs), one LDS-DMA piece
     // (gap 4ks+2: K_{j+1} pieces, then V_j pieces), and with SM2 the second softmax half of the
@@ -1006,29 +1027,29 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                 else dma_one_at<(2 + c) * T + (ks - NP) * 1024>(vr, lds_base, vvo[ks - NP], ks == NP);
             }
             if constexpr (do_sm) {
-                static_for<32>([&](auto U) {
+                static_for<kNL>([&](auto U) {
                     constexpr int u = decltype(U)::value;
-                    if constexpr ((u * G1) / 32 == g) {
-                        u_exp(pr, u & 1, 1, u >> 1);
-                        if constexpr (u >= 2) u_fin(pr, u & 1, 1, (u >> 1) - 1);
+                    if constexpr ((u * G1) / kNL == g) {
+                        u_exp(pr, u & 1, Late::hf(u), Late::v(u));
+                        if constexpr (u >= 2) u_fin(pr, u & 1, Late::hf(u - 2), Late::v(u - 2));
                     }
                 });
             }
             FA_SCHED_FENCE();
         });
         if constexpr (do_sm) {
-            u_fin(pr, 0, 1, 15);
-            u_fin(pr, 1, 1, 15);
+            u_fin(pr, 0, Late::hf(kNL - 2), Late::v(kNL - 2));
+            u_fin(pr, 1, Late::hf(kNL - 1), Late::v(kNL - 1));
         }
     };
     // the same second softmax half without MFMAs (drain and masked tiles)
     auto sm2_all = [&](auto PAR) __attribute__((always_inline)) {
         constexpr int c = decltype(PAR)::value;
-        static_for<16>([&](auto VV) {
-            constexpr int v = decltype(VV)::value;
+        static_for<32 - kV0>([&](auto VV) {  // the late scores
+            constexpr int q = kV0 + decltype(VV)::value;
             static_for<2>([&](auto XX) {
-                u_exp(c, decltype(XX)::value, 1, v);
-                u_fin(c, decltype(XX)::value, 1, v);
+                u_exp(c, decltype(XX)::value, q >> 4, q & 15);
+                u_fin(c, decltype(XX)::value, q >> 4, q & 15);
             });
         });
     };
@@ -1040,12 +1061,22 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     constexpr int G2 = 4 * NPK;
     constexpr int GQ = G2 / 8;  // 4 (D=128) / 2 (D=64)
     // exp unit e (0..31) -> block / score: A0..A4, then B and A alternating, then B11..B15
-    struct Ex {  // exp unit e (0..31) -> block / score: A0..A4, then B and A alternating, then B11..B15
-        static constexpr int blk(int e) { return e < 5 ? 0 : (e < 27 ? (((e - 5) & 1) ? 0 : 1) : 1); }
-        static constexpr int v(int e) {
-            return e < 5 ? e : (e < 27 ? (((e - 5) & 1) ? 5 + ((e - 5) >> 1) : (e - 5) >> 1) : 11 + (e - 27));
+    constexpr int NE = 2 * kV0;  // early exp units of phase 2
+    struct Ex {  // early exp unit e (0..NE-1) -> block / score: A0..A3, then B and A alternating, then B's tail
+        // head: A's units before B's first one, which waits for B's rescale decision
+        static constexpr int hd() {
+            int hh = 4;
+            while (GQ + 2 + (hh * (G2 - GQ - 2)) / NE < 2 * GQ + 1) ++hh;
+            return hh;
         }
-        static constexpr int gap(int e) { return GQ + 2 + (e * (G2 - GQ - 2)) / 32; }
+        static constexpr int mid() { return 2 * (kV0 - hd()); }
+        static constexpr int blk(int e) { return e < hd() ? 0 : (e < hd() + mid() ? (((e - hd()) & 1) ? 0 : 1) : 1); }
+        static constexpr int v(int e) {  // score index q = 16 * half + v
+            return e < hd() ? e
+                            : (e < hd() + mid() ? (((e - hd()) & 1) ? hd() + ((e - hd()) >> 1) : (e - hd()) >> 1)
+                                                : (kV0 - hd()) + (e - hd() - mid()));
+        }
+        static constexpr int gap(int e) { return GQ + 2 + (e * (G2 - GQ - 2)) / NE; }
         static constexpr int max_gap(int X, int m) { return X * GQ + (m * GQ) / 16; }
         static constexpr int dec_gap(int X, int k) { return (X + 1) * GQ + (GQ == 2 ? 0 : k); }
     };
@@ -1054,9 +1085,11 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             if (Ex::dec_gap(X, 0) < Ex::max_gap(X, 15) || Ex::dec_gap(X, 1) < Ex::dec_gap(X, 0)) return false;
             if (Ex::max_gap(X, 15) >= G2) return false;
         }
-        for (int e = 0; e < 32; ++e) {
+        int seen[2][32] = {};
+        for (int e = 0; e < NE; ++e) {
             if (Ex::gap(e) < Ex::dec_gap(Ex::blk(e), 1) || Ex::gap(e) >= G2) return false;
             if (e > 0 && Ex::gap(e) < Ex::gap(e - 1)) return false;
+            if (Ex::v(e) < 0 || Ex::v(e) >= kV0 || seen[Ex::blk(e)][Ex::v(e)]++) return false;  // v: score index q
         }
         return true;
     }(), "phase-2 softmax schedule");
@@ -1095,18 +1128,18 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                     constexpr int X2 = decltype(K2)::value >> 1, k = decltype(K2)::value & 1;
                     if constexpr (Ex::dec_gap(X2, k) == g) u_dec(cs, X2, k);
                 });
-                static_for<32>([&](auto E) {
+                static_for<NE>([&](auto E) {
                     constexpr int e = decltype(E)::value;
-                    if constexpr (Ex::gap(e) + 1 == g) u_fin(cs, Ex::blk(e), 0, Ex::v(e));
-                    if constexpr (Ex::gap(e) == g) u_exp(cs, Ex::blk(e), 0, Ex::v(e));
+                    if constexpr (Ex::gap(e) + 1 == g) u_fin(cs, Ex::blk(e), Ex::v(e) >> 4, Ex::v(e) & 15);
+                    if constexpr (Ex::gap(e) == g) u_exp(cs, Ex::blk(e), Ex::v(e) >> 4, Ex::v(e) & 15);
                 });
             }
             FA_SCHED_FENCE();
         });
         if constexpr (do_sm) {
-            static_for<32>([&](auto E) {
+            static_for<NE>([&](auto E) {
                 constexpr int e = decltype(E)::value;
-                if constexpr (Ex::gap(e) == G2 - 1) u_fin(cs, Ex::blk(e), 0, Ex::v(e));
+                if constexpr (Ex::gap(e) == G2 - 1) u_fin(cs, Ex::blk(e), Ex::v(e) >> 4, Ex::v(e) & 15);
             });
         }
     };
@@ -1118,9 +1151,10 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             static_for<16>([&](auto M) { u_max(c, X, decltype(M)::value); });
             u_dec(c, X, 0);
             u_dec(c, X, 1);
-            static_for<16>([&](auto VV) {
-                u_exp(c, X, 0, decltype(VV)::value);
-                u_fin(c, X, 0, decltype(VV)::value);
+            static_for<kV0>([&](auto VV) {  // the early scores (the late ones: sm2_all)
+                constexpr int q = decltype(VV)::value;
+                u_exp(c, X, q >> 4, q & 15);
+                u_fin(c, X, q >> 4, q & 15);
             });
         });
     };

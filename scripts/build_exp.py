@@ -7,7 +7,7 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 from flash_attention_cute_amd import _build  # noqa: E402
 
-ONLY = (("F16", 0, 128, 1), ("F16", 1, 128, 1))
+ONLY = (("F16", 0, 128, 1), ("F16", 1, 128, 1), ("BF16", 1, 128, 1))
 
 
 def one(spec):
@@ -15,7 +15,8 @@ def one(spec):
     tag = parts[0]
     defs = tuple(x for x in parts[1].split(",") if x) if len(parts) > 1 else ()
     flags = tuple(parts[2].split()) if len(parts) > 2 else ()
-    return _build.build_abi(stamps=True, tag=tag, defines=defs, flags=flags, only=ONLY, force=True)
+    stamps = not tag.startswith("x")  # tags starting with "x": plain experiment builds (no stamps)
+    return _build.build_abi(stamps=stamps, tag=tag, defines=defs, flags=flags, only=ONLY, force=True)
 
 
 with ThreadPoolExecutor(max_workers=4) as ex:
