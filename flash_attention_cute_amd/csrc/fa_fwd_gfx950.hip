@@ -47,11 +47,15 @@ int64_t fa::w4_grid(int64_t nwg) {
             n = 256;
         if (dev >= 0) cus[dev] = n;
     }
-    int64_t cap = n >= 8 ? n / 8 * 8 : n;
+    int64_t cap = n;
     if (const char *e = getenv("FA_W4_GRID")) {
         const long long v = atoll(e);
         if (v > 0) cap = v;
     }
+    if (nwg <= cap) return nwg;  // one Q block per workgroup
+    // Capped: the kernel deals Q block i to the workgroups with (bid & 7) == (i & 7), so every
+    // residue class needs a workgroup -- at least 8, a multiple of 8 (equal rounds per XCD).
+    cap = cap < 8 ? 8 : cap / 8 * 8;
     return nwg < cap ? nwg : cap;
 }
 

@@ -37,9 +37,9 @@ inline int variant_from_env() {
 // fa_debug_set_stamps in fa_fwd_gfx950.hip and scripts/stamps.py); nullptr otherwise
 unsigned long long *stamp_buffer();
 
-// workgroups of a persistent fa_fwd_w4 launch over nwg Q blocks: min(nwg, CUs of the current
-// device), a multiple of 8 (one round-robin turn over the XCDs) when capped. FA_W4_GRID=<n>
-// overrides the cap (A/B runs; a cap >= nwg gives the one-block-per-workgroup launch).
+// workgroups of a persistent fa_fwd_w4 launch over nwg Q blocks: nwg if it fits the cap (the CU
+// count of the current device), else the cap rounded down to a multiple of 8, at least 8 (the kernel
+// deals Q blocks to workgroups by bid mod 8). FA_W4_GRID=<n> overrides the cap (A/B runs, tests).
 int64_t w4_grid(int64_t nwg);
 
 // launch one (dtype, causal, head-dim tile, exact head dim) instantiation on `stream`

@@ -4,5 +4,5 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
 for t in $1; do
   echo "=== $t"
-  FA_STAMPS_LIB=build/stamps_$t/libfa_gfx950.so timeout -k 10 60 python scripts/stamps.py ${2:-c2} 2>&1 | grep -E "per tile|clock|total " || exit 1
+  FA_STAMPS_LIB=build/stamps_$t/libfa_gfx950.so timeout -k 10 60 python scripts/stamps.py ${2:-c2} 2>&1 | grep -E "per tile|clock|total |p50" || exit 1
 done

@@ -217,3 +217,26 @@ def test_full_size_configs_sampled(fa, device):
             vs = v[bi:bi + 1, kh:kh + 1].cpu()
             check(out[bi:bi + 1, h:h + 1], qs, ks, vs, 128 ** -0.5, causal, dtype)
         del q, k, v, out
+
+
+@pytest.mark.parametrize("grid", ["1", "5", "8", "13", "20", "64"])
+def test_persistent_grid_sizes(device, grid, monkeypatch):
+    """fa_fwd_w4 is persistent (a workgroup walks Q blocks, snake-ordered rounds per XCD residue
+    class); forcing small grids (FA_W4_GRID, rounded by the host to >= 8 / multiples of 8) must
+    cover every block and give the default launch's output bit for bit."""
+    import flash_attention_cute_amd as m
+
+    monkeypatch.setenv("FA_GFX950_VARIANT", "w4")
+    cases = [(2, 8, 2, 700, 700, 128, torch.float16, True), (3, 6, 6, 513, 640, 64, torch.bfloat16, False),
+             (1, 12, 4, 1100, 1100, 96, torch.float16, True)]
+    for i, (b, hq, hkv, sq, sk, d, dt, causal) in enumerate(cases):
+        q, k, v = make(b, hq, hkv, sq, sk, d, dt, 300 + i)
+        qd, kd, vd = (t.to(device) for t in (q, k, v))
+        monkeypatch.delenv("FA_W4_GRID", raising=False)
+        ref = m.flash_attn_func(qd, kd, vd, causal=causal)
+        monkeypatch.setenv("FA_W4_GRID", grid)
+        got = m.flash_attn_func(qd, kd, vd, causal=causal)
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref), (grid, i, (got.float() - ref.float()).abs().max().item())
+        if i == 0:
+            check(got, q, k, v, d ** -0.5, causal, dt)
