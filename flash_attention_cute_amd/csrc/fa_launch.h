@@ -53,9 +53,10 @@ constexpr int kDecKeys = 32;  // keys per tile
 constexpr int kDecWaves = 4;  // waves per workgroup, each on its own contiguous key range
 // decode kernel when a (batch, kv-head) has at most this many (q-head, position) rows
 constexpr int kDecMaxRows = 2 * kDecRows;
-// split plan: about one workgroup per CU (the 128 KiB LDS ring admits one), every wave at least
-// kDecMinTilesPerWave tiles
-constexpr int kDecTargetWgs = 256;
+// split plan: about kDecTargetWgs workgroups (the 128 KiB LDS ring admits one per CU), every wave
+// at least kDecMinTilesPerWave tiles. Fewer, longer splits than one per CU measured faster (B1 Hkv8
+// Sk131072 bf16: 5.2-5.5 TB/s at 160-192 workgroups vs 4.9-5.0 at 256, same run)
+constexpr int kDecTargetWgs = 160;
 constexpr int kDecMinTilesPerWave = 4;
 constexpr int kDecMaxSplit = 64;
 
