@@ -132,8 +132,11 @@ int fa_abi_version(void);
 
 /*
  * Tile geometry of the kernel that fa_fwd_gfx950 would launch for these
- * parameters: rows of q per workgroup, keys per KV tile, threads per
- * workgroup and number of workgroups. Host-only, for schedulers and tests.
+ * parameters: rows of q per work unit, keys per KV tile, threads per
+ * workgroup and number of work units (Q blocks; decode: row blocks x key
+ * splits). The prefill kernel is persistent: it launches min(units, CUs)
+ * workgroups that walk the units (FA_W4_GRID overrides the cap). Host-only
+ * (touches no device), for schedulers and tests.
  */
 int fa_fwd_gfx950_geometry(const fa_fwd_params *params, int causal, int64_t *block_m,
                            int64_t *block_n, int64_t *threads, int64_t *workgroups);
