@@ -240,3 +240,33 @@ def test_persistent_grid_sizes(device, grid, monkeypatch):
         assert torch.equal(got, ref), (grid, i, (got.float() - ref.float()).abs().max().item())
         if i == 0:
             check(got, q, k, v, d ** -0.5, causal, dt)
+
+
+@pytest.mark.parametrize("shape", [(2, 8, 2, 640, 640, 128, True), (4, 32, 8, 1, 3000, 128, False)])
+def test_hip_graph_capture_replay(device, shape):
+    """The op launches asynchronously on the caller's stream with no host sync, so it can be
+    captured into a HIP graph (torch.cuda.CUDAGraph) and replayed: prefill (persistent fa_fwd_w4)
+    and Sq == 1 decode (split-KV kernel + combine, stream-ordered workspace)."""
+    import flash_attention_cute_amd as m
+
+    b, hq, hkv, sq, sk, d, causal = shape
+    q, k, v = (t.to(device) for t in make(b, hq, hkv, sq, sk, d, torch.float16, 77))
+    ref = m.flash_attn_func(q, k, v, causal=causal)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):  # warm-up on the side stream, as torch's graph docs prescribe
+        m.flash_attn_func(q, k, v, causal=causal)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = m.flash_attn_func(q, k, v, causal=causal)
+    for seed in (78, 79):  # replay on new inputs written in place
+        q2, k2, v2 = make(b, hq, hkv, sq, sk, d, torch.float16, seed)
+        q.copy_(q2)
+        k.copy_(k2)
+        v.copy_(v2)
+        g.replay()
+        torch.cuda.synchronize()
+        eager = m.flash_attn_func(q, k, v, causal=causal)
+        assert torch.equal(out, eager)
+    assert not torch.equal(out, ref)
