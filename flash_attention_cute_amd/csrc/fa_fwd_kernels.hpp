@@ -527,7 +527,6 @@ __device__ __forceinline__ void agpr_mfma(const u32x4 &a, const u32x4 &b) {
         else fa_agpr_mfma_bf16_##N(a, b);                             \
     }
     FA_CASE(0) FA_CASE(16) FA_CASE(32) FA_CASE(48) FA_CASE(64) FA_CASE(80) FA_CASE(96) FA_CASE(112)
-    FA_CASE(192) FA_CASE(208)
 #undef FA_CASE
 }
 template <int DTL, bool kBlockB>
@@ -555,15 +554,6 @@ __device__ __forceinline__ f32x16 agpr_read16() {
 #pragma unroll
     for (int i = 0; i < 16; ++i) v[i] = x[i];
     return v;
-}
-template <int BASE>
-__device__ __forceinline__ float agpr_read1() {
-    if constexpr (BASE == 64) return fa_agpr_read1_64();
-    else if constexpr (BASE == 80) return fa_agpr_read1_80();
-    else if constexpr (BASE == 128) return fa_agpr_read1_128();
-    else if constexpr (BASE == 192) return fa_agpr_read1_192();
-    else if constexpr (BASE == 208) return fa_agpr_read1_208();
-    else return fa_agpr_read1_144();
 }
 
 // one MFMA of S^T = K.Q^T into arch VGPRs (inline asm, so hipcc keeps it in program order among
@@ -693,9 +683,8 @@ constexpr int vmcnt_enc(int n) { return (n & 15) | (((n >> 4) & 3) << 14) | 0x70
 // fa_fwd_w4: one wave per SIMD, 64 query rows per wave (two 32-row blocks A and B). Per KV tile j:
 //
 //   P1(j): S_A(j), S_B(j) = K_j . Q^T   (32 MFMAs, K fragments shared)  ||  softmax part 2 of j-1
-//   P2(j): O += V_{j-1}^T . P^T(j-1)    (2*DTL+2 MFMAs per 16 keys: both blocks share the V^T
-//          fragments; the row sums of P ride on an extra MFMA with an all-ones A operand)
-//                                                                      ||  softmax part 1 of j
+//   P2(j): O += V_{j-1}^T . P^T(j-1)    (2*DTL MFMAs per 16 keys: both blocks share the V^T
+//          fragments)                                                  ||  softmax part 1 of j
 //          then (rarely) rescale O and the row sums of a block whose max grew past the threshold
 //
 // MFMAs are inline asm (S into arch VGPRs, O and row sums into literal AGPRs, fa_agpr_asm.inc),
@@ -729,14 +718,6 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // the first k-step of S = K.Q^T accumulates from C = -m*s' (the running reference max,
     // "bias"): S is then already the exp2 argument and a score costs no fma
     constexpr bool kFold = true;
-#endif
-#ifndef FA_LSUM
-    constexpr bool kLsum = false;
-#else
-    // (experiment, off: phase 2 turns MFMA-bound, +2.7% cycles measured) row sums of P by one
-    // extra MFMA per (block, 16-key step) with an all-ones A operand, into a[192 + 16X]: 8 MFMAs
-    // per tile instead of 64 VALU adds
-    constexpr bool kLsum = true;
 #endif
     constexpr int KS = G::kKSteps;
     constexpr int DTL = G::kDTiles;
@@ -887,8 +868,6 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     };
     Sm st[2];
     f32x16 bias[2];  // kFold: -m*s' per lane, the C operand of the first S k-step
-    const uint32_t one2 = F ? 0x3C003C00u : 0x3F803F80u;
-    const u32x4 ones = {one2, one2, one2, one2};  // kLsum: A operand of the row-sum MFMA
     f32x16 S[2][4];  // [tile parity][2 * block + half]: half 0 = keys 0-31, 1 = keys 32-63
     u32x4 P[2][8];   // [tile parity][4 * block + k-step]
 
@@ -961,8 +940,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // P.V operand of its 16-key k-step
     auto u_fin = [&](const int c, const int X, const int hf, const int v) {
         const f32x16 &s = S[c][2 * X + hf];
-        if constexpr (!kLsum) {
-            // half 1 and the late scores of half 0 (run after the tile's rescale) add into l
+        {
+            // the late scores (run after the tile's rescale) add into l, the early ones into t
             float &acc = (16 * hf + v >= kV0) ? st[X].l : st[X].t;
             acc = (hf == 0 && v == 0) ? s[0] : acc + s[v];
             pin(acc);
@@ -974,18 +953,10 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         }
     };
     auto rescale = [&]() {
-        if (st[0].resc) {
-            agpr_scale<DTL, false>(st[0].alpha);
-            if constexpr (kLsum) fa_agpr_scale1_192(st[0].alpha);
-        }
-        if (st[1].resc) {
-            agpr_scale<DTL, true>(st[1].alpha);
-            if constexpr (kLsum) fa_agpr_scale1_208(st[1].alpha);
-        }
-        if constexpr (!kLsum) {
+        if (st[0].resc) agpr_scale<DTL, false>(st[0].alpha);
+        if (st[1].resc) agpr_scale<DTL, true>(st[1].alpha);
 #pragma unroll
-            for (int X = 0; X < 2; ++X) st[X].l = __builtin_fmaf(st[X].l, st[X].alpha, st[X].t);
-        }
+        for (int X = 0; X < 2; ++X) st[X].l = __builtin_fmaf(st[X].l, st[X].alpha, st[X].t);
     };
 
     const uint32_t lds_base = lds_u32(lds) + wave * NP * 1024;  // this wave's pieces of slot 0
@@ -1057,7 +1028,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // ---- phase 2: O^T += V^T.P^T for both blocks (8*DTL single MFMAs into the AGPRs) ----------
     // gap g (kk = g / 2DTL, i = g % 2DTL; MFMA: block i / DTL, d-tile i % DTL): V^T read i of
     // k-step kk+1, and with SM1 the first softmax half of the tile of parity cs (schedule below).
-    constexpr int NPK = 2 * DTL + (kLsum ? 2 : 0);  // MFMAs per 16-key step (+ the row-sum MFMAs)
+    constexpr int NPK = 2 * DTL;  // MFMAs per 16-key step
     constexpr int G2 = 4 * NPK;
     constexpr int GQ = G2 / 8;  // 4 (D=128) / 2 (D=64)
     // exp unit e (0..31) -> block / score: A0..A4, then B and A alternating, then B11..B15
@@ -1108,12 +1079,11 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         static_for<G2>([&](auto G) {
             constexpr int g = decltype(G)::value;
             constexpr int kk = g / NPK, i = g % NPK;
-            constexpr int X = kLsum ? i / (DTL + 1) : i / DTL, dt = kLsum ? i % (DTL + 1) : i % DTL;
+            constexpr int X = i / DTL, dt = i % DTL;
             // one counted wait per 16-key step: its V^T fragments were read in the first DTL gaps
             // of the previous step, two per gap
             if constexpr (kk > 0 && i == 0) __builtin_amdgcn_s_waitcnt(kLgkm0);
-            if constexpr (dt == DTL) agpr_mfma<F, 192 + 16 * X>(ones, P[cp][4 * X + kk]);  // row sums
-            else agpr_mfma<F, X * 16 * DTL + 16 * dt>(va[kk & 1][dt], P[cp][4 * X + kk]);
+            agpr_mfma<F, X * 16 * DTL + 16 * dt>(va[kk & 1][dt], P[cp][4 * X + kk]);
             FA_SCHED_FENCE();  // (see phase 1)
             if constexpr (kk + 1 < 4 && i < DTL) {
                 rd(kk + 1, 2 * i, va[(kk + 1) & 1]);
@@ -1193,7 +1163,6 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         st[X] = {kNeg, 0.f, 1.f, kNeg, kNeg, 0.f, 0.f, 0.f, false, false, false};
         bias[X] = (f32x16){};
     }
-    if constexpr (kLsum) fa_agpr_zero_l();
     if constexpr (DTL == 4) fa_agpr_zero_4(); else fa_agpr_zero_2();
     // tile -1 of the pipeline is empty: its S = kNeg gives P = 0, and its P.V reads V slot 1,
     // zeroed here so that 0 * V stays 0 (the previous block's V may hold non-finite values).
@@ -1374,9 +1343,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         }
     };
     FA_STAMP(s_masked_end);
-    // row sums: the MFMA accumulators hold the full sum (both lane halves); the VALU path sums half
-    const float l0 = kLsum ? agpr_read1<192>() : pair_sum(st[0].l);
-    const float l1 = kLsum ? agpr_read1<208>() : pair_sum(st[1].l);
+    // row sums: each lane half summed half of the tile's keys
+    const float l0 = pair_sum(st[0].l);
+    const float l1 = pair_sum(st[1].l);
     store_block(r, IC<0>{}, l0);
     store_block(r + 32, IC<16 * DTL>{}, l1);
 #ifdef FA_STAMPS
