@@ -191,8 +191,11 @@ def main() -> None:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
     n_gpus = world
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # BENCH_SHARE_GPU=1 (rehearsal only): every rank uses cuda:0, so the multi-rank flow can be run on
+    # a one-GPU box; the numbers of such a run are not scaling numbers
+    gpu = 0 if os.environ.get("BENCH_SHARE_GPU") == "1" else local_rank
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
 
     from flash_attention_cute_amd import flash_attn_func
 
