@@ -11,22 +11,26 @@
 //   reference csrc/flash_attention_impl.cu:7-49          tile choice + 4 specialisations
 //   reference csrc/kernel_dispatcher.h:20-52             dtype / headdim / causal dispatch
 //
-// Design (DESIGN.md section 3 has the numbers):
-//   * one workgroup = 8 wave64s = 256 query rows of one (batch, q-head); each wave owns 32 rows;
-//   * KV tiles of 64 keys are register-staged (global_load_dwordx4 issued one tile ahead)
-//     into a double-buffered LDS ring (K and V, 16 KiB each per buffer, 64 KiB total);
+// Two prefill kernels (DESIGN.md section 4 has the numbers):
+//   * fa_fwd_w4 (default): persistent grid, one workgroup per CU walking Q blocks of 256 query rows
+//     of one (batch, q-head); 4 wave64s, one per SIMD, each owning 64 rows (two 32-row blocks)
+//     with the whole 512-register file: O^T and the Q fragments in literal AGPRs (fa_agpr_asm.inc),
+//     K/V tiles of 64 keys by LDS-DMA into 2-slot rings, a two-phase software pipeline per tile
+//     (S = K.Q^T beside the previous tile's softmax tail; O += P.V beside this tile's max, rescale
+//     decision and first exps) with every MFMA issued alone between hand-placed softmax units;
+//   * fa_fwd_w8 (FA_GFX950_VARIANT=w8, cross-check): 8 wave64s x 32 rows, register-staged K/V.
+// Both:
 //   * S^T = K . Q^T with v_mfma_f32_32x32x16_{f16,bf16}: A = K rows from LDS (ds_read_b128,
-//     XOR-swizzled), B = Q^T held in VGPRs for the whole KV loop. Each lane then owns ONE query
-//     and 32 of the tile's 64 keys, so the row max / row sum are in-lane plus a single
-//     v_permlane32_swap (the reference needs a 4-lane shuffle butterfly, template.cuh:72-88);
+//     XOR-swizzled), B = Q^T. Each lane then owns ONE query and 32 of the tile's 64 keys, so the
+//     row max / row sum are in-lane plus a single v_permlane32_swap (the reference needs a 4-lane
+//     shuffle butterfly, template.cuh:72-88);
 //   * O^T += V^T . P^T with the same MFMA: the S^T accumulator, rounded to T, is directly the
 //     B operand (no LDS round trip, no lane movement); V^T comes from ds_read_b64_tr_b16
 //     transposed LDS reads of a row-major, XOR-swizzled V tile;
 //   * O^T keeps the query on the lane, so the online-softmax rescale is a per-lane scalar;
-//   * masking only on KV tiles that cross the causal diagonal or the Sk tail, and a wave skips
-//     KV tiles that are fully masked for its 32 rows;
-//   * workgroup ids are remapped so that the q-tiles of one kv-head group run on one XCD
-//     (blocks b and b+8 share an XCD), keeping the K/V stream in that XCD's 4 MiB L2.
+//   * masking only on KV tiles that cross the causal diagonal or the Sk tail;
+//   * Q blocks are ordered so that the q-tiles of one kv-head group run on one XCD (blocks b and
+//     b+8 share an XCD), keeping the K/V stream in that XCD's 4 MiB L2; causal orders heavy-first.
 //
 // Numerics follow the reference (Appendix A of SURVEY.md): S accumulated in fp32, max taken on
 // unscaled S, P = exp2(S*s' - m*s') with s' = scale*log2(e) precomputed by the host, P rounded
