@@ -886,6 +886,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // the rescale decision of block X in two units: the row max and m_new; then m*sc and alpha
     auto u_dec = [&](const int c, const int X, const int k) {
         Sm &Z = st[X];
+#ifdef FA_EXP_NODEC
+        if (true) { (void)c; (void)k; Z.resc = false; Z.alpha = 1.f; return; }  // timing only
+#endif
         if constexpr (kFold) {
             // S already holds s*s' - m*s' (bias): the tile max is the rise over the reference
             if (k == 0) {
@@ -915,12 +918,12 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         if (k == 0) {
             const float mx = pair_max(fmaxf(Z.mE, Z.mO));
             Z.resc = __builtin_amdgcn_ballot_w64(mx > Z.m + thr_raw) != 0;
-            Z.mE = Z.resc ? fmaxf(Z.m, mx) : Z.m;
+            Z.mE = mx;
             pin(Z.mE);
-        } else {
-            const float m_new = Z.mE;
+        } else if (__builtin_expect(Z.resc, 0)) {  // wave-uniform and rare: the rest only then
+            const float m_new = fmaxf(Z.m, Z.mE);
             const float seen = m_new > 0.5f * kNeg ? 1.f : 0.f;  // m_new * sc, or 0 before any visible key
-            const float msc_new = Z.resc ? m_new * sc * seen : Z.msc;
+            const float msc_new = m_new * sc * seen;
             // a row's first visible key: O and l are still 0 and exp2(0 - m*sc) may overflow
             Z.alpha = (Z.m <= 0.5f * kNeg) ? 0.f : __builtin_amdgcn_exp2f(Z.msc - msc_new);
             Z.m = m_new;
@@ -957,10 +960,19 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         }
     };
     auto rescale = [&]() {
-        if (st[0].resc) agpr_scale<DTL, false>(st[0].alpha);
-        if (st[1].resc) agpr_scale<DTL, true>(st[1].alpha);
+        // rare: one branch for both blocks (a block that did not rescale has alpha = 1)
+        if (__builtin_expect(st[0].resc || st[1].resc, 0)) {
+            agpr_scale<DTL, false>(st[0].alpha);
+            agpr_scale<DTL, true>(st[1].alpha);
 #pragma unroll
-        for (int X = 0; X < 2; ++X) st[X].l = __builtin_fmaf(st[X].l, st[X].alpha, st[X].t);
+            for (int X = 0; X < 2; ++X) {
+                st[X].l = __builtin_fmaf(st[X].l, st[X].alpha, st[X].t);
+                st[X].alpha = 1.f;
+            }
+        } else {
+#pragma unroll
+            for (int X = 0; X < 2; ++X) st[X].l += st[X].t;
+        }
     };
 
     const uint32_t lds_base = lds_u32(lds) + wave * NP * 1024;  // this wave's pieces of slot 0
