@@ -864,6 +864,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // ---- state ------------------------------------------------------------------------------
     struct Sm {               // online-softmax state of one block (per lane: one query row)
         float m, msc, alpha;  // running max (unscaled), m*sc, alpha of the last decision
+        float mt;             // m + the rescale threshold (unscaled)
         float mE, mO;         // two max chains over the tile being reduced (mE then holds m_new)
         float l, t;           // this lane's half of the row sum over finished tiles; s0 sum of the
                               // tile being reduced (new scale, folded into l at the rescale)
@@ -916,17 +917,20 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             return;
         }
         if (k == 0) {
-            const float mx = pair_max(fmaxf(Z.mE, Z.mO));
-            Z.resc = __builtin_amdgcn_ballot_w64(mx > Z.m + thr_raw) != 0;
+            // both lane halves hold the same row's m, so the ballot over the half-row maxima
+            // needs no cross-half reduction; the row max itself is only needed to rescale
+            const float mx = fmaxf(Z.mE, Z.mO);
+            Z.resc = __builtin_amdgcn_ballot_w64(mx > Z.mt) != 0;
             Z.mE = mx;
             pin(Z.mE);
         } else if (__builtin_expect(Z.resc, 0)) {  // wave-uniform and rare: the rest only then
-            const float m_new = fmaxf(Z.m, Z.mE);
+            const float m_new = fmaxf(Z.m, pair_max(Z.mE));
             const float seen = m_new > 0.5f * kNeg ? 1.f : 0.f;  // m_new * sc, or 0 before any visible key
             const float msc_new = m_new * sc * seen;
             // a row's first visible key: O and l are still 0 and exp2(0 - m*sc) may overflow
             Z.alpha = (Z.m <= 0.5f * kNeg) ? 0.f : __builtin_amdgcn_exp2f(Z.msc - msc_new);
             Z.m = m_new;
+            Z.mt = m_new + thr_raw;
             Z.msc = msc_new;
             pin(Z.msc);
             pin(Z.alpha);
@@ -1176,7 +1180,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     vp = vb;
 #pragma unroll
     for (int X = 0; X < 2; ++X) {
-        st[X] = {kNeg, 0.f, 1.f, kNeg, kNeg, 0.f, 0.f, 0.f, false, false, false};
+        st[X] = {kNeg, 0.f, 1.f, kNeg + thr_raw, kNeg, kNeg, 0.f, 0.f, 0.f, false, false, false};
         bias[X] = (f32x16){};
     }
     if constexpr (DTL == 4) fa_agpr_zero_4(); else fa_agpr_zero_2();
