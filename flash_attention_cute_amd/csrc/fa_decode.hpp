@@ -216,9 +216,9 @@ __global__ __launch_bounds__(256, 1) void fa_decode(const fa_fwd_params p, const
         float mx = fmaxf(s[0], s[1]);
 #pragma unroll
         for (int i = 2; i < 16; ++i) mx = fmaxf(mx, s[i]);
-        mx = pair_max(mx);
+        // both lane halves hold the same row's m_use: the check needs no cross-half reduction
         if (__builtin_amdgcn_ballot_w64(mx > m_use + thr_raw)) {
-            const float m_new = fmaxf(m_use, mx);
+            const float m_new = fmaxf(m_use, pair_max(mx));
             const float msc_new = (m_new <= 0.5f * kNeg) ? 0.f : m_new * sc;
             // a row's first visible key: O and l are still 0, alpha must not overflow
             const float alpha = (m_use <= 0.5f * kNeg) ? 0.f : __builtin_amdgcn_exp2f(msc - msc_new);

@@ -372,13 +372,13 @@ __global__ __launch_bounds__(kThreads) void fa_fwd_w8(const fa_fwd_params p, con
         float mx = fmaxf(fmaxf(s0[0], s0[1]), fmaxf(s1[0], s1[1]));
 #pragma unroll
         for (int i = 2; i < 16; i += 2) mx = fmaxf(mx, fmaxf(fmaxf(s0[i], s0[i + 1]), fmaxf(s1[i], s1[i + 1])));
-        mx = pair_max(mx);
         // deferred rescale: taken by the whole wave when any row's max outgrows m_use; every
-        // earlier P.V is already in O at this point (lag waves ran theirs first)
+        // earlier P.V is already in O at this point (lag waves ran theirs first). Both lane halves
+        // hold the same row's m_use, so the check needs no cross-half reduction.
         float alpha = 1.f;
         const bool grow = mx > m_use + thr_raw;
         if (__builtin_amdgcn_ballot_w64(grow)) {
-            const float m_new = fmaxf(m_use, mx);
+            const float m_new = fmaxf(m_use, pair_max(mx));
             const float msc_new = (m_new <= kNeg) ? 0.f : m_new * sc;
             alpha = __builtin_amdgcn_exp2f(msc - msc_new);  // msc == 0 && m_use == kNeg: l, O are 0
             m_use = m_new;
