@@ -869,6 +869,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         float l, t;           // this lane's half of the row sum over finished tiles; s0 sum of the
                               // tile being reduced (new scale, folded into l at the rescale)
         float delta;          // kFold: rise of the reference m*sc at this tile's decision
+        uint64_t rmask;       // the decision's ballot (rows whose max outgrew m + threshold)
         bool resc, seen, vis; // kFold: the row has seen a visible key; this tile has one
     };
     Sm st[2];
@@ -920,10 +921,15 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             // both lane halves hold the same row's m, so the ballot over the half-row maxima
             // needs no cross-half reduction; the row max itself is only needed to rescale
             const float mx = fmaxf(Z.mE, Z.mO);
-            Z.resc = __builtin_amdgcn_ballot_w64(mx > Z.mt) != 0;
+            // the mask is materialised in SGPRs here, a gap before the branches that test it (a
+            // branch on vcc straight from the compare measured slower)
+            uint64_t bm = __builtin_amdgcn_ballot_w64(mx > Z.mt);
+            asm volatile("" : "+s"(bm));
+            Z.rmask = bm;
+            Z.resc = bm != 0;
             Z.mE = mx;
             pin(Z.mE);
-        } else if (__builtin_expect(Z.resc, 0)) {  // wave-uniform and rare: the rest only then
+        } else if (__builtin_expect(Z.rmask != 0, 0)) {  // wave-uniform and rare: the rest only then
             const float m_new = fmaxf(Z.m, pair_max(Z.mE));
             const float seen = m_new > 0.5f * kNeg ? 1.f : 0.f;  // m_new * sc, or 0 before any visible key
             const float msc_new = m_new * sc * seen;
@@ -965,7 +971,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     };
     auto rescale = [&]() {
         // rare: one branch for both blocks (a block that did not rescale has alpha = 1)
-        if (__builtin_expect(st[0].resc || st[1].resc, 0)) {
+        if (__builtin_expect((st[0].rmask | st[1].rmask) != 0, 0)) {
             agpr_scale<DTL, false>(st[0].alpha);
             agpr_scale<DTL, true>(st[1].alpha);
 #pragma unroll
@@ -1180,7 +1186,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     vp = vb;
 #pragma unroll
     for (int X = 0; X < 2; ++X) {
-        st[X] = {kNeg, 0.f, 1.f, kNeg + thr_raw, kNeg, kNeg, 0.f, 0.f, 0.f, false, false, false};
+        st[X] = {kNeg, 0.f, 1.f, kNeg + thr_raw, kNeg, kNeg, 0.f, 0.f, 0.f, 0ull, false, false, false};
         bias[X] = (f32x16){};
     }
     if constexpr (DTL == 4) fa_agpr_zero_4(); else fa_agpr_zero_2();
