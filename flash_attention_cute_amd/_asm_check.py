@@ -1,0 +1,64 @@
+"""Build gate on the device assembly of every kernel instantiation (called by ``_build.build_abi``).
+
+``fa_fwd_w4`` keeps O (a0..a127) and the Q fragments (a128..a191) in literal AGPRs that only its
+inline asm reads and writes (csrc/fa_agpr_asm.inc). The compiler does not know these registers are
+live across the separate asm statements, so a compiler-generated AGPR use in that range (for example
+a VGPR spill to an AGPR after a toolchain or code change) would silently corrupt the output. This
+module scans the ``-save-temps`` assembly: any use of a0..a191 outside ``;;#ASMSTART``/``;;#ASMEND``
+inside ``fa_fwd_w4``, or any kernel with ``.vgpr_spill_count`` > 0, fails the build.
+
+CLI: ``python -m flash_attention_cute_amd._asm_check file.s [...]``
+"""
+from __future__ import annotations
+
+import re
+import sys
+
+PINNED = 192  # a0..a127 (O) and a128..a191 (Q) belong to the inline asm (fa_agpr_asm.inc)
+_REG = re.compile(r"\ba\[(\d+)(?::\d+)?\]|\ba(\d+)\b")
+
+
+def agpr_violations(text: str) -> list[str]:
+    """Compiler-generated uses of the pinned AGPRs inside fa_fwd_w4 (one entry per offending line)."""
+    bad, in_asm, fn = [], False, None
+    for ln in text.splitlines():
+        m = re.match(r"^(_Z\S*):", ln)
+        if m:
+            fn = m.group(1) if m.group(1).startswith("_ZN2fa9fa_fwd_w4") else None
+            continue
+        if ";;#ASMSTART" in ln:
+            in_asm = True
+        elif ";;#ASMEND" in ln:
+            in_asm = False
+        elif fn and not in_asm and not ln.lstrip().startswith(";"):
+            for r in _REG.finditer(ln.split(";")[0]):
+                if int(r.group(1) or r.group(2)) < PINNED:
+                    bad.append(f"{fn}: {ln.strip()}")
+                    break
+    return bad
+
+
+def spills(text: str) -> list[str]:
+    """Kernels whose metadata reports VGPR spills to memory."""
+    out = []
+    for block in re.split(r"\n\s*- \.", text):
+        name = re.search(r"\.name:\s+(\S+)", block)
+        vs = re.search(r"\.vgpr_spill_count:\s+(\d+)", block)
+        if name and vs and int(vs.group(1)) > 0:
+            out.append(f"{name.group(1)}: vgpr_spill_count {vs.group(1)}")
+    return out
+
+
+def check_file(path) -> list[str]:
+    text = open(path).read()
+    if "fa_fwd_w4" not in text:
+        return [f"{path}: no fa_fwd_w4 kernel in the assembly (stale or wrong file)"]
+    return agpr_violations(text) + spills(text)
+
+
+if __name__ == "__main__":
+    problems = [p for f in sys.argv[1:] for p in check_file(f)]
+    for p in problems[:40]:
+        print(p)
+    print(f"{len(problems)} problems")
+    sys.exit(1 if problems else 0)

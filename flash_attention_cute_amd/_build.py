@@ -57,8 +57,9 @@ def _run(cmd: list[str], verbose: bool) -> None:
 
 
 def abi_sources() -> list[Path]:
-    return [CSRC / "fa_fwd_gfx950.hip", CSRC / "fa_fwd_kernels.hpp", CSRC / "fa_launch.h", CSRC / "fa_inst.hip",
-            CSRC / "fa_agpr_asm.inc", INCLUDE / "fa_gfx950.h", Path(__file__).resolve()]
+    """Every file an instantiation TU or the dispatcher can include (any header edit rebuilds)."""
+    dev = [p for ext in ("*.hip", "*.hpp", "*.h", "*.inc") for p in sorted(CSRC.glob(ext))]
+    return dev + sorted(INCLUDE.glob("*.h")) + [Path(__file__).resolve(), PKG / "_asm_check.py"]
 
 
 # (dtype, causal, head-dim tile, exact head dim): must match FA_FOR_EACH_INSTANCE in csrc/fa_launch.h
@@ -97,19 +98,35 @@ def build_abi(force: bool = False, verbose: bool = False, stamps: bool = False, 
     objdir.mkdir(parents=True, exist_ok=True)
     cmds = []
     objs = []
+    asm_files = []
     for dt, c, d, e in INSTANCES:
-        obj = objdir / f"fa_inst_{dt.lower()}_c{c}_d{d}_x{e}.o"
+        # one directory per instantiation: -save-temps=obj names its files after the source
+        idir = objdir / f"{dt.lower()}_c{c}_d{d}_x{e}"
+        idir.mkdir(parents=True, exist_ok=True)
+        obj = idir / "fa_inst.o"
         objs.append(obj)
         stub = ["-DFA_INST_STUB=1"] if only and (dt, c, d, e) not in only else []
+        if not stub:
+            asm_files.append(idir / f"fa_inst-hip-amdgcn-amd-amdhsa-{ARCH}.s")
         cmds.append([HIPCC, *HIP_FLAGS, *extra, *stub, f"-I{INCLUDE}", f"-I{CSRC}", f"-DFA_INST_DT={dt}",
-                     f"-DFA_INST_CAUSAL={c}", f"-DFA_INST_D={d}", f"-DFA_INST_EXACT={e}", "-c", CSRC / "fa_inst.hip",
-                     "-o", obj])
+                     f"-DFA_INST_CAUSAL={c}", f"-DFA_INST_D={d}", f"-DFA_INST_EXACT={e}", "-save-temps=obj",
+                     "-Wno-inline-asm", "-c", CSRC / "fa_inst.hip", "-o", obj])
     disp = objdir / "fa_fwd_gfx950.o"
     objs.append(disp)
     cmds.append([HIPCC, *HIP_FLAGS, *extra, f"-I{INCLUDE}", f"-I{CSRC}", "-c", CSRC / "fa_fwd_gfx950.hip", "-o", disp])
     with ThreadPoolExecutor(max_workers=_jobs()) as ex:
         for f in [ex.submit(_run, cmd, verbose) for cmd in cmds]:
             f.result()
+    # gate: the literal-AGPR invariant of fa_fwd_w4 and no VGPR spills (_asm_check)
+    from ._asm_check import check_file
+
+    problems = [p for a in asm_files for p in check_file(a)]
+    for a in asm_files:  # keep the .s for inspection, drop the large intermediates
+        for junk in a.parent.glob("fa_inst*"):
+            if junk.suffix in (".bc", ".hipi", ".out", ".txt", ".hipfb") or junk.name.endswith("resolution.txt"):
+                junk.unlink()
+    if problems:
+        raise RuntimeError("device assembly check failed (_asm_check):\n" + "\n".join(problems[:20]))
     tmp = out_lib.with_suffix(".so.tmp")
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp], verbose)
     os.replace(tmp, out_lib)

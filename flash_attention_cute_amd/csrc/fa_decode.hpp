@@ -384,6 +384,7 @@ int launch_decode(const fa_fwd_params &p, DecArgs a, void *ws, hipStream_t strea
                            stream, p, a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "HIP launch failed: %s", hipGetErrorString(e));
+    set_last_path(a.n_split > 1 ? kPathDecodeSplit : kPathDecode);
     return FA_OK;
 }
 

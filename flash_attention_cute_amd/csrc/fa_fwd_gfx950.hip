@@ -32,7 +32,43 @@ int fa::set_err(int code, const char *fmt, ...) {
 
 namespace {
 unsigned long long *g_stamps = nullptr;
+thread_local int g_last_path = fa::kPathNone;
+
+fa::Knobs knobs_from_env() {
+    fa::Knobs k{0, 0, 1, fa::kDecTargetWgs, fa::kDecNt};
+    if (const char *v = getenv("FA_GFX950_VARIANT")) k.variant = !strcmp(v, "w8") ? 1 : !strcmp(v, "w4slow") ? 2 : 0;
+    if (const char *e = getenv("FA_W4_GRID")) k.w4_grid = atoll(e) > 0 ? atoll(e) : 0;
+    if (const char *e = getenv("FA_GFX950_DECODE")) k.decode = strcmp(e, "0") != 0;
+    if (const char *e = getenv("FA_DEC_TARGET_WGS")) k.dec_target = atoll(e) > 0 ? atoll(e) : fa::kDecTargetWgs;
+    if (const char *e = getenv("FA_DEC_FLAGS")) k.dec_flags = atoi(e);
+    return k;
+}
+const fa::Knobs &env_defaults() {
+    static const fa::Knobs d = knobs_from_env();  // once per process, at the first launch
+    return d;
+}
+fa::Knobs &knobs_mut() {
+    static fa::Knobs k = env_defaults();
+    return k;
+}
 }  // namespace
+
+const fa::Knobs &fa::knobs() { return knobs_mut(); }
+void fa::set_last_path(int path) { g_last_path = path; }
+
+// Diagnostic hooks (not in include/fa_gfx950.h; flash_attention_cute_amd/_debug.py):
+// override the knobs for the following launches (a negative value restores that knob's
+// environment/default value) and report the kernel the last call on this thread launched.
+extern "C" void fa_debug_set_knobs(int variant, int64_t w4_grid, int decode, int64_t dec_target, int dec_flags) {
+    const fa::Knobs &d = env_defaults();
+    fa::Knobs &k = knobs_mut();
+    k.variant = variant < 0 ? d.variant : variant;
+    k.w4_grid = w4_grid < 0 ? d.w4_grid : w4_grid;
+    k.decode = decode < 0 ? d.decode : decode;
+    k.dec_target = dec_target <= 0 ? d.dec_target : dec_target;
+    k.dec_flags = dec_flags < 0 ? d.dec_flags : dec_flags;
+}
+extern "C" int fa_debug_last_path(void) { return g_last_path; }
 
 unsigned long long *fa::stamp_buffer() { return g_stamps; }
 
@@ -48,10 +84,7 @@ int64_t fa::w4_grid(int64_t nwg) {
         if (dev >= 0) cus[dev] = n;
     }
     int64_t cap = n;
-    if (const char *e = getenv("FA_W4_GRID")) {
-        const long long v = atoll(e);
-        if (v > 0) cap = v;
-    }
+    if (fa::knobs().w4_grid > 0) cap = fa::knobs().w4_grid;
     if (nwg <= cap) return nwg;  // one Q block per workgroup
     // Capped: the kernel deals Q block i to the workgroups with (bid & 7) == (i & 7), so every
     // residue class needs a workgroup -- at least 8, a multiple of 8 (equal rounds per XCD).
@@ -125,12 +158,10 @@ int launch_dec(const fa_fwd_params &p, const fa::DecArgs &a, void *ws, hipStream
 }
 
 // Split-KV decode path (fa_decode.hpp) for few (q-head, position) rows per (batch, kv-head): the
-// reference's Sq == 1 pack and short GQA query blocks. FA_GFX950_DECODE=0 sends them to the
-// prefill kernel instead (A/B measurements).
+// reference's Sq == 1 pack and short GQA query blocks. The `decode` knob (FA_GFX950_DECODE=0) sends
+// them to the prefill kernel instead (A/B measurements).
 bool use_decode(const fa_fwd_params &p) {
-    const char *e = getenv("FA_GFX950_DECODE");
-    if (e && strcmp(e, "0") == 0) return false;
-    if (fa::variant_from_env() != 0) return false;
+    if (!fa::knobs().decode || fa::knobs().variant != 0) return false;
     if (p.head_q_per_group * p.seqlen_q > fa::kDecMaxRows) return false;
     // the row block's q rows are addressed by 32-bit offsets from the group's first q-head
     const int64_t qspan = ((p.head_q_per_group - 1) * p.q_head_stride + (p.seqlen_q - 1) * p.q_seqlen_stride +
@@ -139,6 +170,7 @@ bool use_decode(const fa_fwd_params &p) {
 }
 
 int dispatch(const fa_fwd_params *params, int dtype, int causal, void *ws, int64_t ws_bytes, void *stream) {
+    g_last_path = fa::kPathNone;
     const int rc = check_params(params, dtype, causal);
     if (rc != FA_OK) return rc;
     hipStream_t s = (hipStream_t)stream;

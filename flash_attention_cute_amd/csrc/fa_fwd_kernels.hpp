@@ -1413,6 +1413,7 @@ int launch_one(const fa_fwd_params &p, hipStream_t stream) {
                            (int)n_qtiles, variant == 2 ? 1 : 0, stamp_buffer());
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "HIP launch failed: %s", hipGetErrorString(e));
+    set_last_path(variant == 1 ? kPathW8 : variant == 2 ? kPathW4Slow : kPathW4);
     return FA_OK;
 }
 

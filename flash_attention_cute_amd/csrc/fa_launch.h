@@ -23,15 +23,29 @@ struct BF16;
 // records a message for fa_last_error() and returns `code`
 int set_err(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 
-// Kernel variant: 0 = fa_fwd_w4 (default), 1 = fa_fwd_w8 (FA_GFX950_VARIANT=w8: the 8-wave
-// register-staged kernel, kept for A/B measurements and as a cross-check in the tests),
-// 2 = w4 without its pipelined body (FA_GFX950_VARIANT=w4slow, debug).
-inline int variant_from_env() {
-    const char *v = getenv("FA_GFX950_VARIANT");
-    if (v && strcmp(v, "w8") == 0) return 1;
-    if (v && strcmp(v, "w4slow") == 0) return 2;
-    return 0;
-}
+// Tuning / debug knobs. The product dispatcher never reads the environment per launch: the values
+// are taken ONCE, from the environment of the process at the first launch (A/B scripts set them on
+// the command line), and can be changed afterwards only through fa_debug_set_knobs (tests).
+//   variant    0 = fa_fwd_w4 (default); 1 = fa_fwd_w8 (FA_GFX950_VARIANT=w8: the 8-wave
+//              register-staged kernel, A/B and cross-check); 2 = w4 without its pipelined body
+//              (FA_GFX950_VARIANT=w4slow, debug)
+//   w4_grid    cap of the persistent fa_fwd_w4 grid (FA_W4_GRID; 0 = the CU count)
+//   decode     split-KV decode kernel for few rows per kv-head (FA_GFX950_DECODE=0 turns it off)
+//   dec_target workgroups the decode split plan aims at (FA_DEC_TARGET_WGS)
+//   dec_flags  kDec* bits of the decode kernel (FA_DEC_FLAGS)
+struct Knobs {
+    int variant;
+    int64_t w4_grid;
+    int decode;
+    int64_t dec_target;
+    int dec_flags;
+};
+const Knobs &knobs();
+inline int variant_from_env() { return knobs().variant; }
+
+// Which kernel the last fa_fwd_gfx950* call on this thread launched (fa_debug_last_path)
+enum Path { kPathNone = 0, kPathW4 = 1, kPathW8 = 2, kPathW4Slow = 3, kPathDecode = 4, kPathDecodeSplit = 5 };
+void set_last_path(int path);
 
 // diagnostic per-wave phase stamps of fa_fwd_w4 (only a -DFA_STAMPS=1 build writes them; see
 // fa_debug_set_stamps in fa_fwd_gfx950.hip and scripts/stamps.py); nullptr otherwise
@@ -83,10 +97,8 @@ inline DecArgs decode_plan(const fa_fwd_params &p, int max_split) {
     a.n_rb = (a.rows + kDecRows - 1) / kDecRows;
     const int64_t units = decode_units(p, a);
     const int n_tiles = (int)((p.seqlen_kv + kDecKeys - 1) / kDecKeys);
-    const char *tw = getenv("FA_DEC_TARGET_WGS");  // tuning knob (A/B runs)
-    const int64_t target = tw ? atoll(tw) : kDecTargetWgs;
-    const char *fl = getenv("FA_DEC_FLAGS");
-    a.flags = fl ? atoi(fl) : kDecNt;
+    const int64_t target = knobs().dec_target;
+    a.flags = knobs().dec_flags;
     int64_t ns = (target + units - 1) / units;
     const int64_t by_len = n_tiles / (kDecWaves * kDecMinTilesPerWave);
     ns = ns < by_len ? ns : by_len;

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of the persistent fa_fwd_w4 grid: default cap vs FA_W4_GRID values, per config.
-# usage: bash scripts/ab_grid.sh "c2 c4 c5" "100000 512"
+# usage: bash scripts/dev/ab_grid.sh "c2 c4 c5" "100000 512"
 set -o pipefail
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
 for c in ${1:-c2}; do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Dump the main-loop instruction mix of one kernel instantiation (host-side, no GPU).
-# usage: scripts/asm_loop.sh [DT] [CAUSAL] [D] [EXACT] [kernel-name-regex] [top-N]
+# usage: scripts/dev/asm_loop.sh [DT] [CAUSAL] [D] [EXACT] [kernel-name-regex] [top-N]
 DT=${1:-F16}; C=${2:-0}; DD=${3:-128}; E=${4:-1}
 K=${5:-_ZN2fa9fa_fwd_w4}
 D=/root/repo/build/asm; mkdir -p $D; cd $D

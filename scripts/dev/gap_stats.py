@@ -1,4 +1,4 @@
-"""Per-MFMA-gap instruction mix of a loop listing (build/asm/loop.s from scripts/asm_loop.sh).
+"""Per-MFMA-gap instruction mix of a loop listing (build/asm/loop.s from scripts/dev/asm_loop.sh).
 Issue cost model (MI355X_MICROARCH.md 'vector-instruction ISSUE cost'): trans 8, VALU 4, MFMA 8,
 ds 4 (rough), DMA 25 (measured here), s_nop N -> 4(N+1)/4.. rough."""
 import re

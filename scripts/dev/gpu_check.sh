@@ -5,7 +5,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 echo "== diag"
-timeout -k 10 300 python scripts/diag.py 2>&1 | tee gpurun_out/diag.log || exit 1
+timeout -k 10 300 python scripts/dev/diag.py 2>&1 | tee gpurun_out/diag.log || exit 1
 echo "== smoke"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tee gpurun_out/smoke.log || exit 1
 echo "== pytest"

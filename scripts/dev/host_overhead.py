@@ -1,6 +1,6 @@
 """Host-side cost per call of the public op vs the bare extension vs a captured HIP graph (GPU box).
 
-usage: python scripts/host_overhead.py"""
+usage: python scripts/dev/host_overhead.py"""
 import sys
 import time
 from pathlib import Path

@@ -190,3 +190,48 @@ def test_ws_entry_rejects_small_workspace(lib):
     assert b"workspace" in lib.fa_last_error()
     rc = lib.fa_fwd_gfx950_ws(ctypes.byref(p), 0, 0, ctypes.c_void_p(0x100008), ctypes.c_int64(need), None)
     assert rc == FA_ERR_INVALID_ARGUMENT  # misaligned
+
+
+def test_knobs_are_set_through_the_debug_hook_not_per_launch_env(lib, monkeypatch):
+    """The dispatcher reads its tuning knobs once per process; a variable set later changes
+    nothing, only fa_debug_set_knobs does (flash_attention_cute_amd/_debug.py)."""
+    from flash_attention_cute_amd import _debug
+
+    _debug.set_knobs()
+    monkeypatch.setenv("FA_GFX950_VARIANT", "w8")
+    monkeypatch.setenv("FA_GFX950_DECODE", "0")
+    assert geometry(lib, good_params())[2] == 256          # still fa_fwd_w4 (4 waves)
+    assert geometry(lib, decode_params())[0] == 32         # still the decode kernel
+    with _debug.knobs(variant="w8"):
+        assert geometry(lib, good_params())[2] == 512      # fa_fwd_w8: 8 waves
+        assert geometry(lib, decode_params())[0] == 256    # variants other than w4 never use decode
+    with _debug.knobs(decode=False):
+        assert geometry(lib, decode_params())[0] == 256
+    assert geometry(lib, good_params())[2] == 256 and geometry(lib, decode_params())[0] == 32
+    assert _debug.last_path() == "none"  # host-only calls launch nothing
+
+
+def test_asm_check_detects_pinned_agpr_use_and_spills():
+    from flash_attention_cute_amd import _asm_check as A
+
+    ok = ("_ZN2fa9fa_fwd_w4IXEEv:\n\t;;#ASMSTART\n\tv_mfma_f32_32x32x16_f16 a[0:15], v[0:3], v[4:7], a[0:15]\n"
+          "\t;;#ASMEND\n\tv_accvgpr_write_b32 a200, v1\n\ts_endpgm\n")
+    assert A.agpr_violations(ok) == []
+    bad = ok.replace("a200", "a17")
+    assert len(A.agpr_violations(bad)) == 1
+    other = bad.replace("fa_fwd_w4", "fa_decode")  # only fa_fwd_w4 pins AGPRs
+    assert A.agpr_violations(other) == []
+    meta = "amdhsa.kernels:\n  - .agpr_count: 0\n    .name: k1\n    .vgpr_spill_count: 0\n" \
+           "  - .agpr_count: 0\n    .name: k2\n    .vgpr_spill_count: 3\n"
+    assert A.spills(meta) == ["k2: vgpr_spill_count 3"]
+
+
+def test_build_asm_gate_passes_on_the_built_instantiations():
+    from flash_attention_cute_amd import _asm_check as A
+    from flash_attention_cute_amd import _build
+
+    files = sorted((_build.ROOT / "build" / "obj").glob("*/fa_inst-hip-amdgcn-amd-amdhsa-gfx950.s"))
+    if not files:
+        pytest.skip("no -save-temps assembly (library built elsewhere)")
+    assert len(files) == len(_build.INSTANCES)
+    assert [p for f in files for p in A.check_file(f)] == []

@@ -14,7 +14,6 @@ running max a P is rounded against.
 from __future__ import annotations
 
 import ctypes
-import os
 import zlib
 
 import pytest
@@ -27,13 +26,19 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def fa(device):
-    os.environ["FA_GFX950_VARIANT"] = "w4"
-    os.environ.pop("FA_GFX950_DECODE", None)
+    from flash_attention_cute_amd import _debug
     from flash_attention_cute_amd import flash_attention as fam
     from flash_attention_cute_amd import flash_attn_func
 
     assert fam.flash_attention_cuda is not None, f"gfx950 extension failed to load: {fam._load_error!r}"
-    return flash_attn_func
+    _debug.set_knobs()  # the product defaults (w4 + split-KV decode)
+
+    def run(*a, **kw):
+        out = flash_attn_func(*a, **kw)
+        assert _debug.last_path() in ("decode", "decode_split"), _debug.last_path()
+        return out
+
+    return run
 
 
 DECODE = [  # (B, Hq, Hkv, Sk): Sq == 1, q-head pack
@@ -106,12 +111,13 @@ def test_decode_strided_hf_layout(fa, device, dtype):
 def test_decode_matches_prefill_kernel(fa, device):
     # the same decode step through the decode kernel and through the prefill kernel
     q, k, v = (t.to(device) for t in make(4, 32, 8, 1, 2048, 128, torch.bfloat16, 21))
+    from flash_attention_cute_amd import _debug
+    from flash_attention_cute_amd import flash_attn_func
+
     a = fa(q, k, v)
-    os.environ["FA_GFX950_DECODE"] = "0"
-    try:
-        b = fa(q, k, v)
-    finally:
-        os.environ.pop("FA_GFX950_DECODE")
+    with _debug.knobs(decode=False):
+        b = flash_attn_func(q, k, v)
+        assert _debug.last_path() == "w4"
     assert (a.float() - b.float()).abs().max().item() <= 1.6e-2
 
 
@@ -141,5 +147,8 @@ def test_unsplit_c_abi_entry(fa, device):
     lib.fa_fwd_gfx950.restype = ctypes.c_int
     stream = torch.cuda.current_stream().cuda_stream
     assert lib.fa_fwd_gfx950(ctypes.byref(p), 0, 0, ctypes.c_void_p(stream)) == 0
+    from flash_attention_cute_amd import _debug
+
+    assert _debug.last_path() == "decode"  # no workspace: unsplit
     torch.cuda.synchronize()
     check(od.reshape(b, hkv * g, 1, d), q, k, v, d ** -0.5, False, torch.float16)

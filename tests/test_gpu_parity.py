@@ -29,17 +29,34 @@ pytestmark = pytest.mark.gpu
 TOL = {torch.float16: (2e-3, 2e-3, 1e-4), torch.bfloat16: (1.6e-2, 1.6e-2, 1e-3)}
 
 
-@pytest.fixture(scope="module", params=["w4", "w8", "w4slow"])
+@pytest.fixture(params=["w4", "w8", "w4slow"])
 def fa(device, request):
-    # both kernel variants (include/fa_gfx950.h; FA_GFX950_VARIANT selects at launch time)
-    import os
-
-    os.environ["FA_GFX950_VARIANT"] = request.param
+    """The public op with one kernel variant selected (the product default w4, the 8-wave cross-check
+    w8, the non-pipelined debug body w4slow) through the debug knob hook. Function-scoped: the knobs
+    are restored to their defaults after every test, so no later test inherits a variant."""
     import flash_attention_cute_amd as m
+    from flash_attention_cute_amd import _debug
     from flash_attention_cute_amd import flash_attention as fam
 
     assert fam.flash_attention_cuda is not None, f"gfx950 extension failed to load: {fam._load_error!r}"
-    return m.flash_attn_func
+    _debug.set_knobs(variant=request.param)
+    m.flash_attn_func.variant = request.param
+    try:
+        yield m.flash_attn_func
+    finally:
+        _debug.set_knobs()
+
+
+def assert_path(variant, hq, hkv, sq):
+    """The kernel the last call launched: the decode kernel for few rows per kv-head under the
+    default variant (g * Sq <= 64, the Sq == 1 pack included), else the selected prefill body."""
+    from flash_attention_cute_amd import _debug
+
+    rows = (hq // hkv) * sq if sq > 1 else hq // hkv
+    if variant == "w4" and rows <= 64:
+        assert _debug.last_path() in ("decode", "decode_split"), _debug.last_path()
+    else:
+        assert _debug.last_path() == variant, (_debug.last_path(), variant)
 
 
 def make(b, hq, hkv, sq, sk, d, dtype, seed):
@@ -88,6 +105,7 @@ def test_parity_sweep(fa, device, dtype, causal, shape, d):
     seed = zlib.crc32(repr((shape, d, causal, str(dtype))).encode())
     q, k, v = make(b, hq, hkv, sq, sk, d, dtype, seed)
     out = fa(q.to(device), k.to(device), v.to(device), causal=causal)
+    assert_path(fa.variant, hq, hkv, sq)
     torch.cuda.synchronize()
     check(out, q, k, v, d ** -0.5, causal, dtype)
 
@@ -220,22 +238,23 @@ def test_full_size_configs_sampled(fa, device):
 
 
 @pytest.mark.parametrize("grid", ["1", "5", "8", "13", "20", "64"])
-def test_persistent_grid_sizes(device, grid, monkeypatch):
+def test_persistent_grid_sizes(device, grid):
     """fa_fwd_w4 is persistent (a workgroup walks Q blocks, snake-ordered rounds per XCD residue
-    class); forcing small grids (FA_W4_GRID, rounded by the host to >= 8 / multiples of 8) must
-    cover every block and give the default launch's output bit for bit."""
+    class); forcing small grids (the w4_grid knob, rounded by the host to >= 8 / multiples of 8)
+    must cover every block and give the default launch's output bit for bit."""
     import flash_attention_cute_amd as m
+    from flash_attention_cute_amd import _debug
 
-    monkeypatch.setenv("FA_GFX950_VARIANT", "w4")
     cases = [(2, 8, 2, 700, 700, 128, torch.float16, True), (3, 6, 6, 513, 640, 64, torch.bfloat16, False),
              (1, 12, 4, 1100, 1100, 96, torch.float16, True)]
     for i, (b, hq, hkv, sq, sk, d, dt, causal) in enumerate(cases):
         q, k, v = make(b, hq, hkv, sq, sk, d, dt, 300 + i)
         qd, kd, vd = (t.to(device) for t in (q, k, v))
-        monkeypatch.delenv("FA_W4_GRID", raising=False)
         ref = m.flash_attn_func(qd, kd, vd, causal=causal)
-        monkeypatch.setenv("FA_W4_GRID", grid)
-        got = m.flash_attn_func(qd, kd, vd, causal=causal)
+        assert _debug.last_path() == "w4"
+        with _debug.knobs(w4_grid=int(grid)):
+            got = m.flash_attn_func(qd, kd, vd, causal=causal)
+            assert _debug.last_path() == "w4"
         torch.cuda.synchronize()
         assert torch.equal(got, ref), (grid, i, (got.float() - ref.float()).abs().max().item())
         if i == 0:
@@ -248,10 +267,13 @@ def test_hip_graph_capture_replay(device, shape):
     captured into a HIP graph (torch.cuda.CUDAGraph) and replayed: prefill (persistent fa_fwd_w4)
     and Sq == 1 decode (split-KV kernel + combine, stream-ordered workspace)."""
     import flash_attention_cute_amd as m
+    from flash_attention_cute_amd import _debug
 
     b, hq, hkv, sq, sk, d, causal = shape
     q, k, v = (t.to(device) for t in make(b, hq, hkv, sq, sk, d, torch.float16, 77))
     ref = m.flash_attn_func(q, k, v, causal=causal)
+    # the product path, not a variant left behind by another test: w4, or split-KV decode + combine
+    assert _debug.last_path() == ("decode_split" if sq == 1 else "w4"), _debug.last_path()
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):  # warm-up on the side stream, as torch's graph docs prescribe

@@ -57,6 +57,7 @@ def run_layer(attn_cls, cfg, dev, dtype, seqs=(7, 1, 1), patch=False, seed=0):
     total = sum(seqs)
     x = torch.randn(2, total, cfg.hidden_size, device=dev, dtype=dtype)
     outs, pos = [], 0
+    paths = []  # kernel launched per step (patched GPU runs): flash_attention_cute_amd._debug
     ctx = patched(attn_cls) if patch else _null()
     with ctx, torch.no_grad(), warnings.catch_warnings():
         warnings.simplefilter("ignore")
@@ -67,8 +68,14 @@ def run_layer(attn_cls, cfg, dev, dtype, seqs=(7, 1, 1), patch=False, seed=0):
             o, _ = layer(x[:, pos:pos + s], position_embeddings=pe, attention_mask=None, past_key_values=cache,
                          cache_position=pid[0])
             outs.append(o)
+            if patch and torch.device(dev).type == "cuda":
+                from flash_attention_cute_amd import _debug
+
+                paths.append(_debug.last_path())
             pos += s
-    return torch.cat(outs, dim=1)
+    out = torch.cat(outs, dim=1)
+    run_layer.paths = paths
+    return out
 
 
 class _null:
@@ -148,8 +155,15 @@ def test_patch_attn_entry_points_swap_forward():
 def test_patch_gqa_layer_matches_hf_on_gpu(device, attn_cls, mk, dtype):
     cfg = mk(hq=8, hkv=2, d=128)
     seqs = (300, 1, 1, 37)  # prefill, two decode steps (q-head pack), a chunk with Sq < Sk
+    from flash_attention_cute_amd import _debug
+
+    _debug.set_knobs()  # product defaults
     ref = run_layer(attn_cls, cfg, device, torch.float32, seqs=seqs, patch=False)
     got = run_layer(attn_cls, cfg, device, dtype, seqs=seqs, patch=True)
+    # prefill on the pipelined w4 kernel; the Sq == 1 steps on the decode kernel; the 37-row chunk
+    # (4 q-heads x 37 rows > 64) on w4
+    assert run_layer.paths[0] == "w4" and run_layer.paths[3] == "w4", run_layer.paths
+    assert all(p_ in ("decode", "decode_split") for p_ in run_layer.paths[1:3]), run_layer.paths
     # the last chunk (Sq < Sk): unpatched HF SDPA with attention_mask=None uses is_causal only when
     # q_len > 1 and Sq == Sk; compare prefill + decode rows, and the chunk against a bottom-right ref
     tol = 2e-2 if dtype == torch.bfloat16 else 4e-3
