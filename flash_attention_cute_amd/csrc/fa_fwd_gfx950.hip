@@ -143,10 +143,12 @@ int check_params(const fa_fwd_params *p, int dtype, int causal) {
 // head-dim dispatch: D <= 64 runs the 64-wide tile, 64 < D <= 128 the 128-wide tile (the reference
 // runs every D <= 128 on its 128 kernel, csrc/kernel_dispatcher.h:45-52)
 template <class DT, bool C>
-int launch(const fa_fwd_params &p, hipStream_t stream) {
+int launch(const fa_fwd_params &p, hipStream_t stream, const int *cu_q = nullptr, const int *cu_k = nullptr) {
     if (p.headdim <= 64)
-        return p.headdim == 64 ? launch_one<DT, C, 64, true>(p, stream) : launch_one<DT, C, 64, false>(p, stream);
-    return p.headdim == 128 ? launch_one<DT, C, 128, true>(p, stream) : launch_one<DT, C, 128, false>(p, stream);
+        return p.headdim == 64 ? launch_one<DT, C, 64, true>(p, cu_q, cu_k, stream)
+                               : launch_one<DT, C, 64, false>(p, cu_q, cu_k, stream);
+    return p.headdim == 128 ? launch_one<DT, C, 128, true>(p, cu_q, cu_k, stream)
+                            : launch_one<DT, C, 128, false>(p, cu_q, cu_k, stream);
 }
 template <class DT, bool C>
 int launch_dec(const fa_fwd_params &p, const fa::DecArgs &a, void *ws, hipStream_t stream) {
@@ -189,7 +191,38 @@ int dispatch(const fa_fwd_params *params, int dtype, int causal, void *ws, int64
     return causal ? launch<fa::BF16, true>(p, s) : launch<fa::BF16, false>(p, s);
 }
 
+int check_varlen(const fa_varlen_params *v, int dtype, int causal) {
+    if (!v) return set_err(FA_ERR_INVALID_ARGUMENT, "params is NULL");
+    if (!v->cu_seqlens_q || !v->cu_seqlens_k)
+        return set_err(FA_ERR_INVALID_ARGUMENT, "cu_seqlens_q and cu_seqlens_k must be non-NULL");
+    if (((uintptr_t)v->cu_seqlens_q & 3) || ((uintptr_t)v->cu_seqlens_k & 3))
+        return set_err(FA_ERR_INVALID_ARGUMENT, "cu_seqlens must be 4-byte aligned int32 arrays");
+    // packed layout: the batch strides are not used (a sequence starts at row cu_seqlens[b])
+    fa_fwd_params p = v->base;
+    p.q_batch_stride = p.k_batch_stride = p.v_batch_stride = p.o_batch_stride = 0;
+    return check_params(&p, dtype, causal);
+}
+
+int dispatch_varlen(const fa_varlen_params *v, int dtype, int causal, void *stream) {
+    g_last_path = fa::kPathNone;
+    const int rc = check_varlen(v, dtype, causal);
+    if (rc != FA_OK) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    const int *cq = v->cu_seqlens_q, *ck = v->cu_seqlens_k;
+    if (dtype == FA_DTYPE_F16)
+        return causal ? launch<fa::F16, true>(v->base, s, cq, ck) : launch<fa::F16, false>(v->base, s, cq, ck);
+    return causal ? launch<fa::BF16, true>(v->base, s, cq, ck) : launch<fa::BF16, false>(v->base, s, cq, ck);
+}
+
 }  // namespace
+
+extern "C" int fa_fwd_gfx950_varlen(const fa_varlen_params *params, int dtype, int causal, void *stream) {
+    return dispatch_varlen(params, dtype, causal, stream);
+}
+
+extern "C" int fa_fwd_gfx950_varlen_check(const fa_varlen_params *params, int dtype, int causal) {
+    return check_varlen(params, dtype, causal);
+}
 
 extern "C" int fa_fwd_gfx950_check(const fa_fwd_params *params, int dtype, int causal) {
     return check_params(params, dtype, causal);

@@ -702,7 +702,7 @@ constexpr int vmcnt_enc(int n) { return (n & 15) | (((n >> 4) & 3) << 14) | 0x70
 // =============================================================================================
 template <class DT, bool kCausal, int kD, bool kExactD>
 __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const int n_qtiles, const int dbg,
-                                                    unsigned long long *stamps) {
+                                                    unsigned long long *stamps, const int *cu_q, const int *cu_k) {
     // Diagnostic build only (-DFA_STAMPS=1, scripts/stamps.py): per-wave s_memtime phase totals.
 #ifdef FA_STAMPS
     unsigned long long st_t0 = __builtin_amdgcn_s_memtime(), st_rt0 = __builtin_amdgcn_s_memrealtime();
@@ -749,11 +749,14 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     const int r = lane & 31;
     const int h = lane >> 5;
 
-    const int Sq = (int)p.seqlen_q, Sk = (int)p.seqlen_kv, D = (int)p.headdim;
+    // sequence lengths of the current Q block: fixed for a dense launch; per batch row for varlen
+    // (cu_q / cu_k != nullptr: [B + 1] prefix sums, packed rows, p.seqlen_* = the maxima)
+    const int D = (int)p.headdim;
+    int Sq = (int)p.seqlen_q, Sk = (int)p.seqlen_kv;
     const float sc = p.softmax_scale;
     const float thr_raw = kRescaleThr / sc;
-    const int diag = Sk - Sq;
-    const int n_blocks = (Sk + kBlockN - 1) / kBlockN;
+    int diag = Sk - Sq;
+    int n_blocks = (Sk + kBlockN - 1) / kBlockN;
 
     // ---- persistent schedule ----------------------------------------------------------------
     // The grid holds about one workgroup per CU; each walks Q blocks (q-tile, q-head, batch) of its
@@ -777,10 +780,23 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         const Work wk = decode_work<kCausal>(nwg, xcd + 8 * k, n_qtiles, (int)p.num_heads_q);
         const int hq = wk.hq, b = wk.b;
         const int hkv = hq / (int)p.head_q_per_group;
-        qb = (const char *)p.q_ptr + 2 * ((int64_t)b * p.q_batch_stride + (int64_t)hq * p.q_head_stride);
-        kb = (const char *)p.k_ptr + 2 * ((int64_t)b * p.k_batch_stride + (int64_t)hkv * p.k_head_stride);
-        vb = (const char *)p.v_ptr + 2 * ((int64_t)b * p.v_batch_stride + (int64_t)hkv * p.v_head_stride);
-        ob = (char *)p.o_ptr + 2 * ((int64_t)b * p.o_batch_stride + (int64_t)hq * p.o_head_stride);
+        int64_t qrow0 = (int64_t)b * p.q_batch_stride, krow0 = (int64_t)b * p.k_batch_stride;
+        int64_t vrow0 = (int64_t)b * p.v_batch_stride, orow0 = (int64_t)b * p.o_batch_stride;
+        if (cu_q) {  // varlen: batch row b is rows [cu[b], cu[b + 1]) of the packed tensors
+            const int q0 = cu_q[b], k0 = cu_k[b];
+            Sq = cu_q[b + 1] - q0;
+            Sk = cu_k[b + 1] - k0;
+            diag = Sk - Sq;
+            n_blocks = (Sk + kBlockN - 1) / kBlockN;
+            qrow0 = (int64_t)q0 * p.q_seqlen_stride;
+            orow0 = (int64_t)q0 * p.o_seqlen_stride;
+            krow0 = (int64_t)k0 * p.k_seqlen_stride;
+            vrow0 = (int64_t)k0 * p.v_seqlen_stride;
+        }
+        qb = (const char *)p.q_ptr + 2 * (qrow0 + (int64_t)hq * p.q_head_stride);
+        kb = (const char *)p.k_ptr + 2 * (krow0 + (int64_t)hkv * p.k_head_stride);
+        vb = (const char *)p.v_ptr + 2 * (vrow0 + (int64_t)hkv * p.v_head_stride);
+        ob = (char *)p.o_ptr + 2 * (orow0 + (int64_t)hq * p.o_head_stride);
         m0 = wk.qtile * kBlockM;
         mw = m0 + wave * 64;  // block A: rows mw..mw+31, block B: rows mw+32..mw+63
         n_end = n_blocks;
@@ -789,6 +805,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             const int nb = x <= 0 ? 0 : (x + kBlockN - 1) / kBlockN;
             n_end = min(nb, n_blocks);
         }
+        if (m0 >= Sq) n_end = 0;  // varlen: a q-tile past this sequence's end is empty
         // leading tiles with no masked score for any row of the WORKGROUP (pipelined; the same
         // count for all waves keeps the LDS ring and the barriers aligned)
         n_pipe = Sk / kBlockN;
@@ -1313,7 +1330,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // Every wave is past this block's last barrier: the Q AGPRs and both K slots are free (the
     // drain reads only a V slot).
     char *const ob_c = ob;
-    const int mw_c = mw;
+    const int mw_c = mw, sq_c = Sq;
 #ifdef FA_STAMPS
     const uint32_t blk_c = xcd + 8 * kblk;
 #endif
@@ -1338,7 +1355,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // ---- epilogue ---------------------------------------------------------------------------
     mfma_drain();  // last asm MFMA -> AGPR reads
     const int os_ = (int)p.o_seqlen_stride;
-    const rsrc_t orr = make_rsrc(ob_c + 2 * (int64_t)mw_c * os_, slab_bytes(min(Sq - mw_c, 64), os_, D));
+    const rsrc_t orr = make_rsrc(ob_c + 2 * (int64_t)mw_c * os_, slab_bytes(min(sq_c - mw_c, 64), os_, D));
     auto store_block = [&](const int row, auto OBASE, const float l_tot) {
         constexpr int ob0 = decltype(OBASE)::value;
         f32x16 o[DTL];
@@ -1400,17 +1417,18 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 
 // ---- host launch of one instantiation -------------------------------------------------
 template <class DT, bool C, int kD, bool kExact>
-int launch_one(const fa_fwd_params &p, hipStream_t stream) {
+int launch_one(const fa_fwd_params &p, const int *cu_q, const int *cu_k, hipStream_t stream) {
     const int64_t n_qtiles = (p.seqlen_q + kBlockM - 1) / kBlockM;
     const int64_t nwg = n_qtiles * p.num_heads_q * p.batch_size;
-    const int variant = variant_from_env();
+    // varlen always runs fa_fwd_w4 (w4slow under the debug variant); fa_fwd_w8 is dense only
+    const int variant = cu_q && variant_from_env() == 1 ? 0 : variant_from_env();
     if (variant == 1)
         hipLaunchKernelGGL((fa_fwd_w8<DT, C, kD, kExact>), dim3((uint32_t)nwg), dim3(kThreads), 0, stream, p,
                            (int)n_qtiles);
     else
         // persistent: about one workgroup per CU (the kernel walks the Q blocks itself)
         hipLaunchKernelGGL((fa_fwd_w4<DT, C, kD, kExact>), dim3((uint32_t)w4_grid(nwg)), dim3(256), 0, stream, p,
-                           (int)n_qtiles, variant == 2 ? 1 : 0, stamp_buffer());
+                           (int)n_qtiles, variant == 2 ? 1 : 0, stamp_buffer(), cu_q, cu_k);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "HIP launch failed: %s", hipGetErrorString(e));
     set_last_path(variant == 1 ? kPathW8 : variant == 2 ? kPathW4Slow : kPathW4);

@@ -56,9 +56,10 @@ unsigned long long *stamp_buffer();
 // deals Q blocks to workgroups by bid mod 8). FA_W4_GRID=<n> overrides the cap (A/B runs, tests).
 int64_t w4_grid(int64_t nwg);
 
-// launch one (dtype, causal, head-dim tile, exact head dim) instantiation on `stream`
+// launch one (dtype, causal, head-dim tile, exact head dim) instantiation on `stream`; cu_q / cu_k
+// (device, [B + 1] prefix sums of the per-sequence lengths) select the varlen layout, or nullptr
 template <class DT, bool C, int kD, bool kExact>
-int launch_one(const fa_fwd_params &p, hipStream_t stream);
+int launch_one(const fa_fwd_params &p, const int *cu_q, const int *cu_k, hipStream_t stream);
 
 
 // ---- split-KV decode (fa_decode.hpp) -------------------------------------------------------------
@@ -129,7 +130,7 @@ int launch_decode(const fa_fwd_params &p, DecArgs a, void *ws, hipStream_t strea
     X(BF16, true, 128, false) X(BF16, true, 128, true)
 
 #define FA_DECLARE_EXTERN(DT, C, D, E)                                                  \
-    extern template int launch_one<DT, C, D, E>(const fa_fwd_params &, hipStream_t);   \
+    extern template int launch_one<DT, C, D, E>(const fa_fwd_params &, const int *, const int *, hipStream_t); \
     extern template int launch_decode<DT, C, D, E>(const fa_fwd_params &, DecArgs, void *, hipStream_t);
 FA_FOR_EACH_INSTANCE(FA_DECLARE_EXTERN)
 #undef FA_DECLARE_EXTERN

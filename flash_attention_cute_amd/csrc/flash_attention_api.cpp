@@ -170,10 +170,94 @@ torch::Tensor flash_attention_fwd(torch::Tensor &q, torch::Tensor &k, torch::Ten
     return o;
 }
 
+// Variable-length (packed) batches: q [total_q, Hq, D], k / v [total_k, Hkv, D], cu_seqlens_* int32
+// [B + 1] on the device (include/fa_gfx950.h fa_fwd_gfx950_varlen). No reference counterpart
+// (varlen is a TODO at reference README.md:18); the checks follow flash_attention_fwd's.
+torch::Tensor flash_attention_varlen_fwd(torch::Tensor &q, torch::Tensor &k, torch::Tensor &v,
+                                         torch::Tensor &cu_seqlens_q, torch::Tensor &cu_seqlens_k,
+                                         int64_t max_seqlen_q, int64_t max_seqlen_k, float softmax_scale,
+                                         bool causal) {
+    TORCH_CHECK(q.dim() == 3 && k.dim() == 3 && v.dim() == 3, "varlen q, k, v must be 3-D [total, heads, dim]");
+    TORCH_CHECK(k.size(0) == v.size(0), "k, v must have the same number of rows");
+    TORCH_CHECK(k.size(1) == v.size(1), "k, v must have the same number of heads");
+    TORCH_CHECK(q.size(2) == k.size(2) && q.size(2) == v.size(2), "q, k, v must have the same hidden dimension");
+    TORCH_CHECK(q.size(1) > 0 && k.size(1) > 0 && q.size(2) > 0, "q, k, v must have at least one head");
+    TORCH_CHECK(q.size(1) % k.size(1) == 0, "number of heads in q must be multiple of number of heads in k and v");
+    TORCH_CHECK(q.dtype() == k.dtype() && q.dtype() == v.dtype(), "q, k, v must have the same data type");
+    TORCH_CHECK(q.dtype() == torch::kHalf || q.dtype() == torch::kBFloat16,
+                "q, k, v only support fp16 or bf16 data type");
+    TORCH_CHECK(q.stride(2) == 1 && k.stride(2) == 1 && v.stride(2) == 1,
+                "q, k, v must be contiguous in the last dimension");
+    TORCH_CHECK(q.size(2) % 8 == 0, "hidden dimension must be multiple of 8");
+    TORCH_CHECK(q.size(2) <= 128, "only support hidden dimension <= 128");
+    TORCH_CHECK(q.is_cuda() && k.is_cuda() && v.is_cuda(), "q, k, v must be on CUDA device");
+    TORCH_CHECK(q.device() == k.device() && q.device() == v.device(), "q, k, v must be on the same CUDA device");
+    TORCH_CHECK(cu_seqlens_q.dtype() == torch::kInt32 && cu_seqlens_k.dtype() == torch::kInt32,
+                "cu_seqlens must be int32");
+    TORCH_CHECK(cu_seqlens_q.dim() == 1 && cu_seqlens_k.dim() == 1 && cu_seqlens_q.size(0) == cu_seqlens_k.size(0) &&
+                    cu_seqlens_q.size(0) >= 2,
+                "cu_seqlens_q and cu_seqlens_k must be 1-D with batch_size + 1 entries");
+    TORCH_CHECK(cu_seqlens_q.device() == q.device() && cu_seqlens_k.device() == q.device(),
+                "cu_seqlens must be on the same device as q");
+    TORCH_CHECK(max_seqlen_q >= 0 && max_seqlen_k >= 0, "max_seqlen must be non-negative");
+
+    c10::DeviceGuard device_guard(q.device());
+    TORCH_CHECK(device_is_gfx950(q.device().index()),
+                "flash attention (gfx950 build) is only supported on MI355X / gfx950 devices");
+    auto o = torch::empty_like(q);
+    if (q.size(0) == 0 || max_seqlen_q == 0) return o;
+    if (max_seqlen_k == 0) return o.zero_();  // no sequence has a key: every row is 0
+
+    auto aligned_rows = [](const torch::Tensor &t) {
+        return reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0 && (t.stride(0) % 8 == 0 || t.size(0) <= 1) &&
+               (t.stride(1) % 8 == 0 || t.size(1) <= 1);
+    };
+    torch::Tensor qx = aligned_rows(q) ? q : q.contiguous();
+    torch::Tensor kx = aligned_rows(k) ? k : k.contiguous();
+    torch::Tensor vx = aligned_rows(v) ? v : v.contiguous();
+    if (!aligned_rows(o)) o = torch::empty(q.sizes(), q.options());
+    torch::Tensor cq = cu_seqlens_q.contiguous(), ck = cu_seqlens_k.contiguous();
+
+    fa_varlen_params vp;
+    fa_fwd_params &params = vp.base;
+    params.q_ptr = qx.data_ptr();
+    params.k_ptr = kx.data_ptr();
+    params.v_ptr = vx.data_ptr();
+    params.o_ptr = o.data_ptr();
+    params.batch_size = cq.size(0) - 1;
+    params.num_heads_q = qx.size(1);
+    params.num_heads_kv = kx.size(1);
+    params.seqlen_q = max_seqlen_q;
+    params.seqlen_kv = max_seqlen_k;
+    params.headdim = qx.size(2);
+    params.head_q_per_group = qx.size(1) / kx.size(1);
+    params.q_batch_stride = params.k_batch_stride = params.v_batch_stride = params.o_batch_stride = 0;
+    params.q_head_stride = qx.stride(1);
+    params.k_head_stride = kx.stride(1);
+    params.v_head_stride = vx.stride(1);
+    params.o_head_stride = o.stride(1);
+    params.q_seqlen_stride = qx.stride(0);
+    params.k_seqlen_stride = kx.stride(0);
+    params.v_seqlen_stride = vx.stride(0);
+    params.o_seqlen_stride = o.stride(0);
+    softmax_scale *= M_LOG2E;
+    params.softmax_scale = softmax_scale;
+    vp.cu_seqlens_q = cq.data_ptr<int32_t>();
+    vp.cu_seqlens_k = ck.data_ptr<int32_t>();
+
+    const int dtype = qx.scalar_type() == torch::kHalf ? FA_DTYPE_F16 : FA_DTYPE_BF16;
+    void *stream = c10::hip::getCurrentHIPStream(qx.device().index()).stream();
+    const int rc = fa_fwd_gfx950_varlen(&vp, dtype, causal ? 1 : 0, stream);
+    TORCH_CHECK(rc == FA_OK, "fa_fwd_gfx950_varlen failed (code ", rc, "): ", fa_last_error());
+    return o;
+}
+
 }  // namespace flash_attention
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("flash_attention_fwd", &flash_attention::flash_attention_fwd,
           "FlashAttention-2 forward, hand-written HIP kernel for MI355X / gfx950");
+    m.def("flash_attention_varlen_fwd", &flash_attention::flash_attention_varlen_fwd,
+          "FlashAttention-2 forward over packed variable-length sequences (cu_seqlens), gfx950");
     m.def("abi_version", []() { return fa_abi_version(); });
 }

@@ -14,6 +14,11 @@ registrations, default-scale rule and wrapper behaviour:
 
 GPU tensors always go through the hand-written HIP kernel: if the extension failed to load, the
 "cuda" kernel raises instead of falling back to a PyTorch implementation.
+
+Beyond the reference (its README.md:18 lists varlen as a TODO): ``flash_attention::varlen_forward``
+/ ``flash_attn_varlen_func`` over packed variable-length sequences described by int32 ``cu_seqlens``
+prefix sums (the layout a padding mask is lowered to; ``hf_attention`` does that lowering), with the
+same registrations (CPU default, "cuda" kernel, fake) and the same pad / contiguity wrapper.
 """
 from __future__ import annotations
 
@@ -72,3 +77,78 @@ def flash_attn_func(q, k, v, softmax_scale=None, causal=False):
     # q: [batch_size, n_heads, q_seq_len, d]; k, v: [batch_size, n_heads_kv, kv_seq_len, d]
     softmax_scale = (q.size(-1) ** -0.5) if softmax_scale is None else softmax_scale
     return torch.ops.flash_attention.forward(q, k, v, softmax_scale, causal)
+
+
+# ---------------------------------------------------------------------------------------------
+# variable-length (packed) sequences -- no reference counterpart (reference README.md:18 TODO)
+# ---------------------------------------------------------------------------------------------
+def _bottom_right_causal(sq: int, sk: int, device) -> torch.Tensor:
+    """[sq, sk] bool, True = visible: key n is visible to query m iff n <= m + sk - sq
+    (the kernel's causal convention, reference csrc/mask.cuh:37-39)."""
+    m = torch.arange(sq, device=device)[:, None]
+    n = torch.arange(sk, device=device)[None, :]
+    return n <= m + (sk - sq)
+
+
+@torch.library.custom_op("flash_attention::varlen_forward", mutates_args=())
+def flash_attention_varlen_forward(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_seqlens_q: torch.Tensor,
+                                   cu_seqlens_k: torch.Tensor, max_seqlen_q: int, max_seqlen_k: int,
+                                   softmax_scale: float = None, causal: bool = False) -> torch.Tensor:
+    # q: [total_q, n_heads, d]; k, v: [total_k, n_heads_kv, d]; cu_seqlens_*: int32 [batch_size + 1].
+    # Non-GPU default: per-sequence torch SDPA with the kernel's semantics (bottom-right causal,
+    # GQA, rows that see no key are 0).
+    warnings.warn("Flash Attention only support cuda now, fallback to pytorch implementation.", stacklevel=2)
+    out = torch.zeros_like(q)
+    cq, ck = cu_seqlens_q.tolist(), cu_seqlens_k.tolist()
+    for b in range(len(cq) - 1):
+        q0, q1, k0, k1 = cq[b], cq[b + 1], ck[b], ck[b + 1]
+        if q1 == q0 or k1 == k0:
+            continue
+        qs, ks, vs = (t.transpose(0, 1).unsqueeze(0) for t in (q[q0:q1], k[k0:k1], v[k0:k1]))
+        mask = _bottom_right_causal(q1 - q0, k1 - k0, q.device) if causal else None
+        o = torch.nn.functional.scaled_dot_product_attention(qs, ks, vs, attn_mask=mask, scale=softmax_scale,
+                                                             enable_gqa=True)
+        if causal:  # rows with no visible key (Sq_b > Sk_b) are 0, as on the GPU
+            o = o.masked_fill(~mask.any(dim=1)[None, None, :, None], 0)
+        out[q0:q1] = o[0].transpose(0, 1)
+    return out
+
+
+@torch.library.register_kernel("flash_attention::varlen_forward", "cuda")
+def flash_attention_varlen_forward_cuda(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
+                                        cu_seqlens_q: torch.Tensor, cu_seqlens_k: torch.Tensor, max_seqlen_q: int,
+                                        max_seqlen_k: int, softmax_scale: float = None,
+                                        causal: bool = False) -> torch.Tensor:
+    if flash_attention_cuda is None:
+        raise RuntimeError(f"gfx950 flash attention extension is not available: {_load_error!r}")
+    head_dim = q.size(2)
+    need_padding = head_dim % 8 != 0
+    if need_padding:
+        pad = [0, 8 - head_dim % 8]
+        q = torch.nn.functional.pad(q, pad)
+        k = torch.nn.functional.pad(k, pad)
+        v = torch.nn.functional.pad(v, pad)
+    q = q.contiguous() if q.stride(2) != 1 else q
+    k = k.contiguous() if k.stride(2) != 1 else k
+    v = v.contiguous() if v.stride(2) != 1 else v
+    attn = flash_attention_cuda.flash_attention_varlen_fwd(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q,
+                                                           max_seqlen_k, softmax_scale, causal)
+    if need_padding:
+        attn = attn[:, :, :head_dim]
+    return attn
+
+
+@torch.library.register_fake("flash_attention::varlen_forward")
+def flash_attention_varlen_forward_fake(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k,
+                                        softmax_scale=None, causal=False):
+    return torch.empty_like(q)
+
+
+def flash_attn_varlen_func(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, softmax_scale=None,
+                           causal=False):
+    """Attention over packed sequences: q [total_q, Hq, D], k/v [total_k, Hkv, D]; sequence b owns rows
+    [cu_seqlens_q[b], cu_seqlens_q[b+1]) of q and [cu_seqlens_k[b], cu_seqlens_k[b+1]) of k/v
+    (int32, on q's device). ``max_seqlen_q`` / ``max_seqlen_k`` must be the true maxima."""
+    softmax_scale = (q.size(-1) ** -0.5) if softmax_scale is None else softmax_scale
+    return torch.ops.flash_attention.varlen_forward(q, k, v, cu_seqlens_q, cu_seqlens_k, int(max_seqlen_q),
+                                                    int(max_seqlen_k), softmax_scale, causal)

@@ -28,7 +28,7 @@ from typing import Optional, Tuple
 import torch
 from torch import nn
 
-from .flash_attention import flash_attn_func
+from .flash_attention import _bottom_right_causal, flash_attn_func, flash_attn_varlen_func
 
 
 def rotate_half(x: torch.Tensor) -> torch.Tensor:
@@ -47,11 +47,75 @@ def apply_rotary_pos_emb(q, k, cos, sin, position_ids=None, unsqueeze_dim=1):
     return q * cos + rotate_half(q) * sin, k * cos + rotate_half(k) * sin
 
 
+def key_padding(attention_mask: Optional[torch.Tensor], sq: int, sk: int, causal: bool) -> Optional[torch.Tensor]:
+    """Lower an HF attention mask to per-token validity ``[B, Sk]`` (True = real token), or None when it
+    masks nothing beyond the plain causal mask.
+
+    Accepted: a 2-D padding mask ``[B, Sk]`` (1 = real token), or the 4-D mask HF builds for SDPA /
+    eager ``[B, 1, Sq, Sk]`` (bool, True = attend; or additive float, 0 = attend) that is exactly
+    "causal (bottom-right) AND key not padding" on every real query row. A query row is real iff
+    its own token (key position m + Sk - Sq) is. Any other mask (sliding / chunked / custom) raises
+    NotImplementedError instead of being silently ignored as in the reference
+    (models/rope_attn_fwd.py:40-64 drops ``attention_mask``).
+    """
+    if attention_mask is None:
+        return None
+    if sq > sk:
+        raise NotImplementedError("flash_attention_cute_amd: attention_mask with more queries than keys")
+    m = attention_mask
+    if m.dim() == 2:
+        if tuple(m.shape[1:]) != (sk,):
+            raise NotImplementedError(f"flash_attention_cute_amd: 2-D attention_mask of shape {tuple(m.shape)} "
+                                      f"does not cover the {sk} keys")
+        kv_valid = m.bool()
+    elif m.dim() == 4:
+        if m.shape[1] != 1 or m.shape[2] != sq or m.shape[3] != sk:
+            raise NotImplementedError(f"flash_attention_cute_amd: 4-D attention_mask of shape {tuple(m.shape)} "
+                                      f"(expected [B, 1, {sq}, {sk}])")
+        m = m[:, 0] if m.dtype == torch.bool else (m[:, 0] == 0)
+        kv_valid = m.any(dim=1)
+        allowed = kv_valid[:, None, :]
+        if causal:
+            allowed = allowed & _bottom_right_causal(sq, sk, m.device)[None]
+        q_valid = kv_valid[:, sk - sq:]
+        if bool(((m != allowed) & q_valid[:, :, None]).any()):
+            raise NotImplementedError("flash_attention_cute_amd: only causal + key-padding attention masks are "
+                                      "supported (this mask masks other scores)")
+    else:
+        raise NotImplementedError(f"flash_attention_cute_amd: attention_mask with {m.dim()} dims")
+    return None if bool(kv_valid.all()) else kv_valid
+
+
+def _varlen_attention(query, key, value, kv_valid, causal, scaling):
+    """Padded batch -> packed sequences -> ``flash_attn_varlen_func`` -> padded [B, Sq, Hq, D] (padding
+    rows 0). q/k/v are [B, H, S, D] views; the valid query rows are the last Sq token positions."""
+    b, hq, sq, d = query.shape
+    hkv, sk = key.shape[1], key.shape[2]
+    q_valid = kv_valid[:, sk - sq:]
+    lens_q = q_valid.sum(1, dtype=torch.int32)
+    lens_k = kv_valid.sum(1, dtype=torch.int32)
+    cu_q = torch.nn.functional.pad(torch.cumsum(lens_q, 0, dtype=torch.int32), (1, 0))
+    cu_k = torch.nn.functional.pad(torch.cumsum(lens_k, 0, dtype=torch.int32), (1, 0))
+    idx_q = q_valid.flatten().nonzero().squeeze(1)
+    idx_k = kv_valid.flatten().nonzero().squeeze(1)
+    qp = query.transpose(1, 2).reshape(b * sq, hq, d).index_select(0, idx_q)
+    kp = key.transpose(1, 2).reshape(b * sk, hkv, d).index_select(0, idx_k)
+    vp = value.transpose(1, 2).reshape(b * sk, hkv, d).index_select(0, idx_k)
+    o = flash_attn_varlen_func(qp, kp, vp, cu_q, cu_k, int(lens_q.max()), int(lens_k.max()), softmax_scale=scaling,
+                               causal=causal)
+    out = query.new_zeros(b * sq, hq, d)
+    out.index_copy_(0, idx_q, o)
+    return out.view(b, sq, hq, d)
+
+
 def _flash_attention_forward(module: nn.Module, query: torch.Tensor, key: torch.Tensor, value: torch.Tensor,
                              attention_mask: Optional[torch.Tensor], dropout: float = 0.0,
                              scaling: Optional[float] = None, sliding_window: Optional[int] = None,
                              softcap: Optional[float] = None, **kwargs) -> Tuple[torch.Tensor, None]:
-    """Attention core (reference models/rope_attn_fwd.py:40-64): returns [B, Sq, Hq, D], None."""
+    """Attention core (reference models/rope_attn_fwd.py:40-64): returns [B, Sq, Hq, D], None.
+
+    Unlike the reference, ``attention_mask`` is honoured: a padding mask runs the varlen kernel
+    over the packed real tokens (``key_padding``); masks it cannot express raise."""
     kwargs.pop("is_causal", None)
     if softcap is not None:
         raise NotImplementedError("flash_attention_cute_amd: attention logit softcapping is not supported")
@@ -62,6 +126,9 @@ def _flash_attention_forward(module: nn.Module, query: torch.Tensor, key: torch.
         raise NotImplementedError(
             f"flash_attention_cute_amd: sliding window {sliding_window} shorter than the {sk} visible keys")
     causal = bool(getattr(module, "is_causal", True)) and sq > 1
+    kv_valid = key_padding(attention_mask, sq, sk, causal)
+    if kv_valid is not None:
+        return _varlen_attention(query, key, value, kv_valid, causal, scaling), None
     attn_output = flash_attn_func(query, key, value, causal=causal, softmax_scale=scaling)
     return attn_output.transpose(1, 2), None
 

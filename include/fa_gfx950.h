@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define FA_GFX950_ABI_VERSION 2
+#define FA_GFX950_ABI_VERSION 3
 
 /* Field order mirrors reference csrc/flash_attention.h:5-37. */
 typedef struct fa_fwd_params {
@@ -140,6 +140,33 @@ int fa_abi_version(void);
  */
 int fa_fwd_gfx950_geometry(const fa_fwd_params *params, int causal, int64_t *block_m,
                            int64_t *block_n, int64_t *threads, int64_t *workgroups);
+
+/*
+ * Variable-length (packed) batches. No reference counterpart: varlen is a TODO at reference
+ * README.md:18, and the reference's vendored models reject any attention_mask
+ * (models/modeling_llama.py:296-297); this is the entry a padding mask is lowered to.
+ *
+ * The B sequences are packed along the row dimension: q [total_q, Hq, D], k/v [total_k, Hkv, D],
+ * o [total_q, Hq, D] (any row / head strides, multiples of 8 elements; last dim contiguous).
+ * Sequence b owns q rows [cu_seqlens_q[b], cu_seqlens_q[b+1]) and k/v rows
+ * [cu_seqlens_k[b], cu_seqlens_k[b+1]) -- int32 prefix sums in DEVICE memory, B + 1 entries.
+ * In `base`: batch_size = B; seqlen_q / seqlen_kv = the maximum per-sequence lengths (seqlen_q sizes
+ * the grid: a longer sequence would be cut short, so the caller must pass the true maximum);
+ * the *_batch_stride fields are ignored; the head / seqlen strides are those of the packed tensors.
+ * Causal masking is bottom-right aligned per sequence (key n visible to query m iff
+ * n <= m + Sk_b - Sq_b), rows of a sequence with no visible key are 0, a sequence with Sk_b == 0
+ * gives 0 rows. The prefill kernel serves every sequence (no split-KV decode path).
+ */
+typedef struct fa_varlen_params {
+    fa_fwd_params base;
+    const int32_t *cu_seqlens_q; /* [B + 1], device */
+    const int32_t *cu_seqlens_k; /* [B + 1], device */
+} fa_varlen_params;
+
+int fa_fwd_gfx950_varlen(const fa_varlen_params *params, int dtype, int causal, void *stream);
+
+/* Host-only validation of the varlen parameters (the device arrays are not read). */
+int fa_fwd_gfx950_varlen_check(const fa_varlen_params *params, int dtype, int causal);
 
 #ifdef __cplusplus
 }

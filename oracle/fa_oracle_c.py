@@ -66,3 +66,22 @@ def forward(q, k, v, softmax_scale: float, causal: bool, threads: int = 0, want_
 
 if __name__ == "__main__":
     print(build(force=bool(os.environ.get("FORCE"))))
+
+
+def forward_varlen(q, k, v, cu_seqlens_q, cu_seqlens_k, softmax_scale: float, causal: bool, threads: int = 0):
+    """Oracle of the varlen entry (include/fa_gfx950.h fa_fwd_gfx950_varlen): packed q [total_q, Hq, D],
+    k/v [total_k, Hkv, D]; each sequence is the dense forward above on its own rows (bottom-right
+    causal per sequence); a sequence without keys gives 0 rows."""
+    import torch
+
+    cq = [int(x) for x in cu_seqlens_q.tolist()]
+    ck = [int(x) for x in cu_seqlens_k.tolist()]
+    q, k, v = (t.detach().cpu() for t in (q, k, v))
+    out = torch.zeros_like(q)
+    for b in range(len(cq) - 1):
+        q0, q1, k0, k1 = cq[b], cq[b + 1], ck[b], ck[b + 1]
+        if q1 == q0 or k1 == k0:
+            continue
+        qs, ks, vs = (t.transpose(0, 1).unsqueeze(0) for t in (q[q0:q1], k[k0:k1], v[k0:k1]))
+        out[q0:q1] = forward(qs, ks, vs, softmax_scale, causal, threads=threads)[0].transpose(0, 1)
+    return out

@@ -41,7 +41,8 @@ def lib():
 def test_header_declares_the_boundary():
     assert set(declared_functions()) == {"fa_fwd_gfx950", "fa_fwd_gfx950_check", "fa_last_error", "fa_abi_version",
                                          "fa_fwd_gfx950_geometry", "fa_fwd_gfx950_ws",
-                                         "fa_fwd_gfx950_workspace_size"}
+                                         "fa_fwd_gfx950_workspace_size", "fa_fwd_gfx950_varlen",
+                                         "fa_fwd_gfx950_varlen_check"}
 
 
 def test_every_declared_symbol_is_exported(lib):
@@ -81,7 +82,7 @@ def check(lib, p, dtype=0, causal=0):
 
 def test_abi_version(lib):
     lib.fa_abi_version.restype = ctypes.c_int
-    assert lib.fa_abi_version() == 2
+    assert lib.fa_abi_version() == 3
 
 
 def test_check_accepts_valid(lib):
@@ -235,3 +236,29 @@ def test_build_asm_gate_passes_on_the_built_instantiations():
         pytest.skip("no -save-temps assembly (library built elsewhere)")
     assert len(files) == len(_build.INSTANCES)
     assert [p for f in files for p in A.check_file(f)] == []
+
+
+class FaVarlenParams(ctypes.Structure):
+    _fields_ = [("base", FaFwdParams), ("cu_seqlens_q", ctypes.c_void_p), ("cu_seqlens_k", ctypes.c_void_p)]
+
+
+def test_varlen_struct_layout():
+    assert ctypes.sizeof(FaVarlenParams) == ctypes.sizeof(FaFwdParams) + 16
+    assert FaVarlenParams.cu_seqlens_q.offset == ctypes.sizeof(FaFwdParams)
+
+
+def test_varlen_check(lib):
+    lib.fa_fwd_gfx950_varlen_check.restype = ctypes.c_int
+    lib.fa_last_error.restype = ctypes.c_char_p
+    base = good_params(q_batch_stride=3, k_batch_stride=5)  # batch strides are ignored by varlen
+    vp = FaVarlenParams(base, 0x50000, 0x60000)
+    assert lib.fa_fwd_gfx950_varlen_check(ctypes.byref(vp), 0, 1) == FA_OK
+    vp = FaVarlenParams(base, None, 0x60000)
+    assert lib.fa_fwd_gfx950_varlen_check(ctypes.byref(vp), 0, 1) == FA_ERR_INVALID_ARGUMENT
+    assert b"cu_seqlens" in lib.fa_last_error()
+    vp = FaVarlenParams(base, 0x50002, 0x60000)
+    assert lib.fa_fwd_gfx950_varlen_check(ctypes.byref(vp), 0, 1) == FA_ERR_INVALID_ARGUMENT
+    vp = FaVarlenParams(good_params(headdim=136), 0x50000, 0x60000)
+    assert lib.fa_fwd_gfx950_varlen_check(ctypes.byref(vp), 0, 1) == FA_ERR_UNSUPPORTED
+    lib.fa_fwd_gfx950_varlen.restype = ctypes.c_int
+    assert lib.fa_fwd_gfx950_varlen(ctypes.byref(vp), 0, 1, None) == FA_ERR_UNSUPPORTED  # validated, no launch
