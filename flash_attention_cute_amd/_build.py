@@ -111,9 +111,10 @@ def build_abi(force: bool = False, verbose: bool = False, stamps: bool = False, 
         cmds.append([HIPCC, *HIP_FLAGS, *extra, *stub, f"-I{INCLUDE}", f"-I{CSRC}", f"-DFA_INST_DT={dt}",
                      f"-DFA_INST_CAUSAL={c}", f"-DFA_INST_D={d}", f"-DFA_INST_EXACT={e}", "-save-temps=obj",
                      "-Wno-inline-asm", "-c", CSRC / "fa_inst.hip", "-o", obj])
-    disp = objdir / "fa_fwd_gfx950.o"
-    objs.append(disp)
-    cmds.append([HIPCC, *HIP_FLAGS, *extra, f"-I{INCLUDE}", f"-I{CSRC}", "-c", CSRC / "fa_fwd_gfx950.hip", "-o", disp])
+    for src in ("fa_fwd_gfx950.hip", "fa_rope.hip"):  # C-ABI dispatcher, standalone RoPE kernel
+        obj = objdir / src.replace(".hip", ".o")
+        objs.append(obj)
+        cmds.append([HIPCC, *HIP_FLAGS, *extra, f"-I{INCLUDE}", f"-I{CSRC}", "-c", CSRC / src, "-o", obj])
     with ThreadPoolExecutor(max_workers=_jobs()) as ex:
         for f in [ex.submit(_run, cmd, verbose) for cmd in cmds]:
             f.result()

@@ -143,12 +143,13 @@ int check_params(const fa_fwd_params *p, int dtype, int causal) {
 // head-dim dispatch: D <= 64 runs the 64-wide tile, 64 < D <= 128 the 128-wide tile (the reference
 // runs every D <= 128 on its 128 kernel, csrc/kernel_dispatcher.h:45-52)
 template <class DT, bool C>
-int launch(const fa_fwd_params &p, hipStream_t stream, const int *cu_q = nullptr, const int *cu_k = nullptr) {
+int launch(const fa_fwd_params &p, hipStream_t stream, const int *cu_q = nullptr, const int *cu_k = nullptr,
+           const fa::RopeArgs &rope = fa::RopeArgs{nullptr, nullptr, 0, 0}) {
     if (p.headdim <= 64)
-        return p.headdim == 64 ? launch_one<DT, C, 64, true>(p, cu_q, cu_k, stream)
-                               : launch_one<DT, C, 64, false>(p, cu_q, cu_k, stream);
-    return p.headdim == 128 ? launch_one<DT, C, 128, true>(p, cu_q, cu_k, stream)
-                            : launch_one<DT, C, 128, false>(p, cu_q, cu_k, stream);
+        return p.headdim == 64 ? launch_one<DT, C, 64, true>(p, cu_q, cu_k, rope, stream)
+                               : launch_one<DT, C, 64, false>(p, cu_q, cu_k, rope, stream);
+    return p.headdim == 128 ? launch_one<DT, C, 128, true>(p, cu_q, cu_k, rope, stream)
+                            : launch_one<DT, C, 128, false>(p, cu_q, cu_k, rope, stream);
 }
 template <class DT, bool C>
 int launch_dec(const fa_fwd_params &p, const fa::DecArgs &a, void *ws, hipStream_t stream) {
@@ -214,7 +215,32 @@ int dispatch_varlen(const fa_varlen_params *v, int dtype, int causal, void *stre
     return causal ? launch<fa::BF16, true>(v->base, s, cq, ck) : launch<fa::BF16, false>(v->base, s, cq, ck);
 }
 
+int dispatch_rope(const fa_rope_fwd_params *r, int dtype, int causal, void *stream) {
+    g_last_path = fa::kPathNone;
+    if (!r) return set_err(FA_ERR_INVALID_ARGUMENT, "params is NULL");
+    const int rc = check_params(&r->base, dtype, causal);
+    if (rc != FA_OK) return rc;
+    if (!r->rope_cos || !r->rope_sin) return set_err(FA_ERR_INVALID_ARGUMENT, "rope_cos and rope_sin must be non-NULL");
+    if (r->base.headdim != 64 && r->base.headdim != 128)
+        return set_err(FA_ERR_UNSUPPORTED, "fused RoPE supports head dim 64 or 128 (got %lld)", (long long)r->base.headdim);
+    if (!aligned16(r->rope_cos) || !aligned16(r->rope_sin) || r->rope_batch_stride % 8 || r->rope_seqlen_stride % 8)
+        return set_err(FA_ERR_INVALID_ARGUMENT, "RoPE tables must be 16-byte aligned with strides multiple of 8");
+    if (r->rope_seqlen_stride < 0 || r->rope_seqlen_stride * 2 * 64 + 256 > 0x7fffffffLL)
+        return set_err(FA_ERR_UNSUPPORTED, "RoPE seqlen stride too large for 32-bit tile offsets");
+    const fa::RopeArgs ra{r->rope_cos, r->rope_sin, r->rope_batch_stride, r->rope_seqlen_stride};
+    hipStream_t s = (hipStream_t)stream;
+    if (dtype == FA_DTYPE_F16)
+        return causal ? launch<fa::F16, true>(r->base, s, nullptr, nullptr, ra)
+                      : launch<fa::F16, false>(r->base, s, nullptr, nullptr, ra);
+    return causal ? launch<fa::BF16, true>(r->base, s, nullptr, nullptr, ra)
+                  : launch<fa::BF16, false>(r->base, s, nullptr, nullptr, ra);
+}
+
 }  // namespace
+
+extern "C" int fa_fwd_gfx950_rope(const fa_rope_fwd_params *params, int dtype, int causal, void *stream) {
+    return dispatch_rope(params, dtype, causal, stream);
+}
 
 extern "C" int fa_fwd_gfx950_varlen(const fa_varlen_params *params, int dtype, int causal, void *stream) {
     return dispatch_varlen(params, dtype, causal, stream);

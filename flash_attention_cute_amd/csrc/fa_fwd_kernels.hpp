@@ -91,6 +91,23 @@ struct F16 {
         return __builtin_bit_cast(uint32_t, v);
     }
     // 8 values * s in fp32, rounded back (RNE)
+    // rotate-half RoPE of 8 elements (HF apply_rotary_pos_emb, reference models/rope_attn_fwd.py:8-38):
+    // x*cos + rot*sin with rot = -partner (first half) / +partner (second half), fp32, one RNE rounding
+    static __device__ __forceinline__ u32x4 rope8(u32x4 v, u32x4 partner, u32x4 c, u32x4 s, bool second) {
+        const f16x8 x = __builtin_bit_cast(f16x8, v), y = __builtin_bit_cast(f16x8, partner);
+        const f16x8 cc = __builtin_bit_cast(f16x8, c), ss = __builtin_bit_cast(f16x8, s);
+        u32x4 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float r0 = second ? (float)y[2 * i] : -(float)y[2 * i];
+            const float r1 = second ? (float)y[2 * i + 1] : -(float)y[2 * i + 1];
+            float a0 = __builtin_fmaf((float)x[2 * i], (float)cc[2 * i], r0 * (float)ss[2 * i]);
+            float a1 = __builtin_fmaf((float)x[2 * i + 1], (float)cc[2 * i + 1], r1 * (float)ss[2 * i + 1]);
+            asm volatile("" : "+v"(a0), "+v"(a1));  // fp32 rounding step kept, as csrc/fa_rope.hip
+            r[i] = pack(a0, a1);
+        }
+        return r;
+    }
     static __device__ __forceinline__ u32x4 scale8(u32x4 v, float s) {
         const f16x8 x = __builtin_bit_cast(f16x8, v);
         u32x4 r;
@@ -110,6 +127,23 @@ struct BF16 {
     static __device__ __forceinline__ uint32_t pack(float lo, float hi) {
         bf16x2 v = __builtin_convertvector((f32x2){lo, hi}, bf16x2);
         return __builtin_bit_cast(uint32_t, v);
+    }
+    // rotate-half RoPE of 8 elements (HF apply_rotary_pos_emb, reference models/rope_attn_fwd.py:8-38):
+    // x*cos + rot*sin with rot = -partner (first half) / +partner (second half), fp32, one RNE rounding
+    static __device__ __forceinline__ u32x4 rope8(u32x4 v, u32x4 partner, u32x4 c, u32x4 s, bool second) {
+        const bf16x8 x = __builtin_bit_cast(bf16x8, v), y = __builtin_bit_cast(bf16x8, partner);
+        const bf16x8 cc = __builtin_bit_cast(bf16x8, c), ss = __builtin_bit_cast(bf16x8, s);
+        u32x4 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float r0 = second ? (float)y[2 * i] : -(float)y[2 * i];
+            const float r1 = second ? (float)y[2 * i + 1] : -(float)y[2 * i + 1];
+            float a0 = __builtin_fmaf((float)x[2 * i], (float)cc[2 * i], r0 * (float)ss[2 * i]);
+            float a1 = __builtin_fmaf((float)x[2 * i + 1], (float)cc[2 * i + 1], r1 * (float)ss[2 * i + 1]);
+            asm volatile("" : "+v"(a0), "+v"(a1));  // fp32 rounding step kept, as csrc/fa_rope.hip
+            r[i] = pack(a0, a1);
+        }
+        return r;
     }
     static __device__ __forceinline__ u32x4 scale8(u32x4 v, float s) {
         const bf16x8 x = __builtin_bit_cast(bf16x8, v);
@@ -702,7 +736,8 @@ constexpr int vmcnt_enc(int n) { return (n & 15) | (((n >> 4) & 3) << 14) | 0x70
 // =============================================================================================
 template <class DT, bool kCausal, int kD, bool kExactD>
 __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const int n_qtiles, const int dbg,
-                                                    unsigned long long *stamps, const int *cu_q, const int *cu_k) {
+                                                    unsigned long long *stamps, const int *cu_q, const int *cu_k,
+                                                    const RopeArgs rope) {
     // Diagnostic build only (-DFA_STAMPS=1, scripts/stamps.py): per-wave s_memtime phase totals.
 #ifdef FA_STAMPS
     unsigned long long st_t0 = __builtin_amdgcn_s_memtime(), st_rt0 = __builtin_amdgcn_s_memrealtime();
@@ -774,6 +809,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 
     // per-block geometry (set_block)
     const char *qb, *kb, *vb;
+    const char *cosb = nullptr, *sinb = nullptr;  // RoPE tables of this block's sequence (rope.cos)
     char *ob;
     int m0, mw, n_end, n_pipe;
     auto set_block = [&](const uint32_t k) {
@@ -792,6 +828,11 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             orow0 = (int64_t)q0 * p.o_seqlen_stride;
             krow0 = (int64_t)k0 * p.k_seqlen_stride;
             vrow0 = (int64_t)k0 * p.v_seqlen_stride;
+        }
+        if (kExactD && rope.cos) {  // (the host only passes RoPE tables to exact-D instantiations)
+            const int64_t crow0 = cu_q ? (int64_t)cu_q[b] * rope.seq_stride : (int64_t)b * rope.batch_stride;
+            cosb = (const char *)rope.cos + 2 * crow0;
+            sinb = (const char *)rope.sin + 2 * crow0;
         }
         qb = (const char *)p.q_ptr + 2 * (qrow0 + (int64_t)hq * p.q_head_stride);
         kb = (const char *)p.k_ptr + 2 * (krow0 + (int64_t)hkv * p.k_head_stride);
@@ -842,7 +883,34 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             });
         }
     };
-    load_q();
+    // RoPE fused into the Q load (rope.cos != nullptr, exact D): Q, cos and sin of the wave's 64 rows
+    // into VGPRs, rotate-half in fp32, rounded once to T, then into the Q AGPRs. The rotation partner
+    // of chunk 2ks+h is chunk 2(ks +- KS/2)+h -- the same lane. Issued in the block prologue (not
+    // under the previous block's drain, whose S / P registers are live) and waited for there.
+    const bool rope_q = kExactD && rope.cos != nullptr;
+    auto load_q_rope = [&]() __attribute__((always_inline)) {
+        const int qs = (int)p.q_seqlen_stride, cs = (int)rope.seq_stride;
+        const int rows = min(Sq - mw, 64);
+        const rsrc_t qr = make_rsrc(qb + 2 * (int64_t)mw * qs, slab_bytes(rows, qs, D));
+        const rsrc_t cr = make_rsrc(cosb + 2 * (int64_t)mw * cs, slab_bytes(rows, cs, D));
+        const rsrc_t sr = make_rsrc(sinb + 2 * (int64_t)mw * cs, slab_bytes(rows, cs, D));
+        static_for<2>([&](auto XX) {
+            constexpr int X = decltype(XX)::value;
+            u32x4 qv[KS], cv[KS], sv[KS];
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                qv[ks] = __builtin_amdgcn_raw_buffer_load_b128(qr, (32 * X + r) * qs * 2 + 32 * ks + 16 * h, 0, 0);
+                cv[ks] = __builtin_amdgcn_raw_buffer_load_b128(cr, (32 * X + r) * cs * 2 + 32 * ks + 16 * h, 0, 0);
+                sv[ks] = __builtin_amdgcn_raw_buffer_load_b128(sr, (32 * X + r) * cs * 2 + 32 * ks + 16 * h, 0, 0);
+            }
+            static_for<KS>([&](auto KK) {
+                constexpr int ks = decltype(KK)::value;
+                constexpr int pk = ks < KS / 2 ? ks + KS / 2 : ks - KS / 2;
+                agpr_qset<QB + 4 * (X * KS + ks)>(DT::rope8(qv[ks], qv[pk], cv[ks], sv[ks], ks >= KS / 2));
+            });
+        });
+    };
+    if (!rope_q) load_q();
 
     // ---- LDS-DMA staging: this wave writes pieces (wave*NP + n) of each K and V tile --------
     const int ks_ = (int)p.k_seqlen_stride, vs_ = (int)p.v_seqlen_stride;
@@ -1201,6 +1269,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #endif
     kp = kb + step_k;
     vp = vb;
+    if (rope_q) load_q_rope();
 #pragma unroll
     for (int X = 0; X < 2; ++X) {
         st[X] = {kNeg, 0.f, 1.f, kNeg + thr_raw, kNeg, kNeg, 0.f, 0.f, 0.f, 0ull, false, false, false};
@@ -1338,7 +1407,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     const bool more = kblk < cnt;
     if (more) {
         set_block(kblk);
-        load_q();
+        if (!rope_q) load_q();
         stage_k(0);
     }
     // drain the last pipelined tile: softmax half 2 and P.V
@@ -1417,18 +1486,19 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 
 // ---- host launch of one instantiation -------------------------------------------------
 template <class DT, bool C, int kD, bool kExact>
-int launch_one(const fa_fwd_params &p, const int *cu_q, const int *cu_k, hipStream_t stream) {
+int launch_one(const fa_fwd_params &p, const int *cu_q, const int *cu_k, const RopeArgs &rope, hipStream_t stream) {
+    if (rope.cos && !kExact) return set_err(FA_ERR_UNSUPPORTED, "fused RoPE needs head dim 64 or 128");
     const int64_t n_qtiles = (p.seqlen_q + kBlockM - 1) / kBlockM;
     const int64_t nwg = n_qtiles * p.num_heads_q * p.batch_size;
-    // varlen always runs fa_fwd_w4 (w4slow under the debug variant); fa_fwd_w8 is dense only
-    const int variant = cu_q && variant_from_env() == 1 ? 0 : variant_from_env();
+    // varlen and fused RoPE always run fa_fwd_w4 (w4slow under the debug variant); w8 has neither
+    const int variant = (cu_q || rope.cos) && variant_from_env() == 1 ? 0 : variant_from_env();
     if (variant == 1)
         hipLaunchKernelGGL((fa_fwd_w8<DT, C, kD, kExact>), dim3((uint32_t)nwg), dim3(kThreads), 0, stream, p,
                            (int)n_qtiles);
     else
         // persistent: about one workgroup per CU (the kernel walks the Q blocks itself)
         hipLaunchKernelGGL((fa_fwd_w4<DT, C, kD, kExact>), dim3((uint32_t)w4_grid(nwg)), dim3(256), 0, stream, p,
-                           (int)n_qtiles, variant == 2 ? 1 : 0, stamp_buffer(), cu_q, cu_k);
+                           (int)n_qtiles, variant == 2 ? 1 : 0, stamp_buffer(), cu_q, cu_k, rope);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "HIP launch failed: %s", hipGetErrorString(e));
     set_last_path(variant == 1 ? kPathW8 : variant == 2 ? kPathW4Slow : kPathW4);

@@ -53,7 +53,65 @@ int64_t stride_or_zero(const torch::Tensor &t, int dim) {
     return t.size(dim) == 1 ? 0 : t.stride(dim);
 }
 
+// cos / sin tables of RoPE: [B, S, D], [1, S, D] or [S, D] of x's dtype on x's device; returns the
+// table as [B', S, D] with 16-B aligned rows (B' = 1: shared by every batch row, batch stride 0)
+torch::Tensor rope_table(const torch::Tensor &t, const torch::Tensor &x, int64_t batch, int64_t seqlen, int64_t dim,
+                         const char *name) {
+    TORCH_CHECK(t.dim() == 2 || t.dim() == 3, name, " must be [B, S, D] or [S, D]");
+    torch::Tensor u = t.dim() == 2 ? t.unsqueeze(0) : t;
+    TORCH_CHECK(u.size(0) == batch || u.size(0) == 1, name, " batch must be 1 or ", batch);
+    TORCH_CHECK(u.size(1) == seqlen && u.size(2) == dim, name, " must cover ", seqlen, " positions x ", dim);
+    TORCH_CHECK(u.dtype() == x.dtype(), name, " must have the dtype of q / k");
+    TORCH_CHECK(u.device() == x.device(), name, " must be on the device of q / k");
+    const bool ok = reinterpret_cast<uintptr_t>(u.data_ptr()) % 16 == 0 && u.stride(2) == 1 &&
+                    (u.stride(1) % 8 == 0 || u.size(1) == 1) && (u.stride(0) % 8 == 0 || u.size(0) == 1);
+    return ok ? u : u.contiguous();
+}
+
+fa_rope_params rope_params(const torch::Tensor &x, const torch::Tensor &out, const torch::Tensor &cs,
+                           const torch::Tensor &sn) {
+    fa_rope_params r;
+    r.x = x.data_ptr();
+    r.out = out.data_ptr();
+    r.cos = cs.data_ptr();
+    r.sin = sn.data_ptr();
+    r.batch_size = x.size(0);
+    r.num_heads = x.size(1);
+    r.seqlen = x.size(2);
+    r.headdim = x.size(3);
+    r.x_batch_stride = x.stride(0);
+    r.x_head_stride = x.stride(1);
+    r.x_seqlen_stride = x.stride(2);
+    r.out_batch_stride = out.stride(0);
+    r.out_head_stride = out.stride(1);
+    r.out_seqlen_stride = out.stride(2);
+    r.cs_batch_stride = cs.size(0) == 1 ? 0 : cs.stride(0);
+    r.cs_seqlen_stride = cs.stride(1);
+    return r;
+}
+
 }  // namespace
+
+// out = x * cos + rotate_half(x) * sin for x [B, H, S, D] (fp16 / bf16, last dim contiguous); out keeps
+// x's strides (HF's [B, S, H, D] projection views stay copy-free). One HIP pass (csrc/fa_rope.hip).
+torch::Tensor rope_apply(torch::Tensor &x, torch::Tensor &cos, torch::Tensor &sin) {
+    TORCH_CHECK(x.dim() == 4, "x must be 4-D [batch, heads, seqlen, dim]");
+    TORCH_CHECK(x.dtype() == torch::kHalf || x.dtype() == torch::kBFloat16, "RoPE supports fp16 or bf16");
+    TORCH_CHECK(x.is_cuda(), "x must be on CUDA device");
+    TORCH_CHECK(x.stride(3) == 1, "x must be contiguous in the last dimension");
+    TORCH_CHECK(x.size(3) % 2 == 0, "RoPE needs an even head dimension");
+    c10::DeviceGuard device_guard(x.device());
+    torch::Tensor cs = rope_table(cos, x, x.size(0), x.size(2), x.size(3), "cos");
+    torch::Tensor sn = rope_table(sin, x, x.size(0), x.size(2), x.size(3), "sin");
+    TORCH_CHECK(cs.size(0) == sn.size(0) && cs.strides() == sn.strides(), "cos and sin must have the same layout");
+    auto out = torch::empty_like(x);
+    if (x.numel() == 0) return out;
+    const fa_rope_params r = rope_params(x, out, cs, sn);
+    const int dtype = x.scalar_type() == torch::kHalf ? FA_DTYPE_F16 : FA_DTYPE_BF16;
+    const int rc = fa_rope_gfx950(&r, dtype, c10::hip::getCurrentHIPStream(x.device().index()).stream());
+    TORCH_CHECK(rc == FA_OK, "fa_rope_gfx950 failed (code ", rc, "): ", fa_last_error());
+    return out;
+}
 
 torch::Tensor flash_attention_fwd(torch::Tensor &q, torch::Tensor &k, torch::Tensor &v, float softmax_scale,
                                   bool causal) {
@@ -170,6 +228,82 @@ torch::Tensor flash_attention_fwd(torch::Tensor &q, torch::Tensor &k, torch::Ten
     return o;
 }
 
+// Attention with RoPE applied to q inside the kernel's Q load (fa_fwd_gfx950_rope); k is already
+// rotated. Query blocks the split-KV decode kernel serves (Sq == 1 pack, g * Sq <= 64) and other head
+// dims rotate q with rope_apply first and take the plain path.
+torch::Tensor flash_attention_rope_fwd(torch::Tensor &q, torch::Tensor &k, torch::Tensor &v, torch::Tensor &cos,
+                                       torch::Tensor &sin, float softmax_scale, bool causal) {
+    TORCH_CHECK(q.dim() == 4 && k.dim() == 4 && v.dim() == 4, "q, k, v must be 4-D [batch, heads, seqlen, dim]");
+    TORCH_CHECK(k.size(1) > 0 && q.size(1) % k.size(1) == 0,
+                "number of heads in q must be multiple of number of heads in k and v");
+    const int64_t g = q.size(1) / k.size(1), sq = q.size(2), d = q.size(3);
+    const bool fused = (d == 64 || d == 128) && sq > 1 && g * sq > 64 && q.is_cuda() && q.stride(3) == 1 &&
+                       (q.dtype() == torch::kHalf || q.dtype() == torch::kBFloat16);
+    if (!fused) {
+        torch::Tensor qr = rope_apply(q, cos, sin);
+        return flash_attention_fwd(qr, k, v, softmax_scale, causal);
+    }
+    // the checks of flash_attention_fwd on a dry run of the same tensors (no Sq == 1 pack here)
+    TORCH_CHECK(q.size(0) == k.size(0) && q.size(0) == v.size(0), "q, k, v must have the same batch size");
+    TORCH_CHECK(k.size(1) == v.size(1), "k, v must have the same number of heads");
+    TORCH_CHECK(k.size(2) == v.size(2), "k, v must have the same sequence length");
+    TORCH_CHECK(q.size(3) == k.size(3) && q.size(3) == v.size(3), "q, k, v must have the same hidden dimension");
+    TORCH_CHECK(k.size(2) > 0 && q.size(0) > 0, "q, k, v must have at least one element");
+    TORCH_CHECK(q.dtype() == k.dtype() && q.dtype() == v.dtype(), "q, k, v must have the same data type");
+    TORCH_CHECK(k.stride(3) == 1 && v.stride(3) == 1, "k, v must be contiguous in the last dimension");
+    TORCH_CHECK(k.is_cuda() && v.is_cuda() && q.device() == k.device() && q.device() == v.device(),
+                "q, k, v must be on the same CUDA device");
+    c10::DeviceGuard device_guard(q.device());
+    TORCH_CHECK(device_is_gfx950(q.device().index()),
+                "flash attention (gfx950 build) is only supported on MI355X / gfx950 devices");
+    torch::Tensor cs = rope_table(cos, q, q.size(0), sq, d, "cos");
+    torch::Tensor sn = rope_table(sin, q, q.size(0), sq, d, "sin");
+    TORCH_CHECK(cs.size(0) == sn.size(0) && cs.strides() == sn.strides(), "cos and sin must have the same layout");
+    torch::Tensor qx = aligned16(q) ? q : q.contiguous();
+    torch::Tensor kx = aligned16(k) ? k : k.contiguous();
+    torch::Tensor vx = aligned16(v) ? v : v.contiguous();
+    auto o = torch::empty_like(qx);
+    if (!aligned16(o)) o = torch::empty(qx.sizes(), qx.options());
+
+    fa_rope_fwd_params rp;
+    fa_fwd_params &params = rp.base;
+    params.q_ptr = qx.data_ptr();
+    params.k_ptr = kx.data_ptr();
+    params.v_ptr = vx.data_ptr();
+    params.o_ptr = o.data_ptr();
+    params.batch_size = qx.size(0);
+    params.num_heads_q = qx.size(1);
+    params.num_heads_kv = kx.size(1);
+    params.seqlen_q = sq;
+    params.seqlen_kv = kx.size(2);
+    params.headdim = d;
+    params.head_q_per_group = g;
+    params.q_batch_stride = stride_or_zero(qx, 0);
+    params.k_batch_stride = stride_or_zero(kx, 0);
+    params.v_batch_stride = stride_or_zero(vx, 0);
+    params.o_batch_stride = stride_or_zero(o, 0);
+    params.q_head_stride = stride_or_zero(qx, 1);
+    params.k_head_stride = stride_or_zero(kx, 1);
+    params.v_head_stride = stride_or_zero(vx, 1);
+    params.o_head_stride = stride_or_zero(o, 1);
+    params.q_seqlen_stride = stride_or_zero(qx, 2);
+    params.k_seqlen_stride = stride_or_zero(kx, 2);
+    params.v_seqlen_stride = stride_or_zero(vx, 2);
+    params.o_seqlen_stride = stride_or_zero(o, 2);
+    softmax_scale *= M_LOG2E;
+    params.softmax_scale = softmax_scale;
+    rp.rope_cos = cs.data_ptr();
+    rp.rope_sin = sn.data_ptr();
+    rp.rope_batch_stride = cs.size(0) == 1 ? 0 : cs.stride(0);
+    rp.rope_seqlen_stride = cs.stride(1);
+    const int dtype = qx.scalar_type() == torch::kHalf ? FA_DTYPE_F16 : FA_DTYPE_BF16;
+    const int rc = fa_fwd_gfx950_rope(&rp, dtype, causal ? 1 : 0,
+                                      c10::hip::getCurrentHIPStream(qx.device().index()).stream());
+    TORCH_CHECK(rc == FA_OK, "fa_fwd_gfx950_rope failed (code ", rc, "): ", fa_last_error());
+    if (o.sizes() != q.sizes()) o = o.reshape(q.sizes());
+    return o;
+}
+
 // Variable-length (packed) batches: q [total_q, Hq, D], k / v [total_k, Hkv, D], cu_seqlens_* int32
 // [B + 1] on the device (include/fa_gfx950.h fa_fwd_gfx950_varlen). No reference counterpart
 // (varlen is a TODO at reference README.md:18); the checks follow flash_attention_fwd's.
@@ -259,5 +393,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           "FlashAttention-2 forward, hand-written HIP kernel for MI355X / gfx950");
     m.def("flash_attention_varlen_fwd", &flash_attention::flash_attention_varlen_fwd,
           "FlashAttention-2 forward over packed variable-length sequences (cu_seqlens), gfx950");
+    m.def("flash_attention_rope_fwd", &flash_attention::flash_attention_rope_fwd,
+          "FlashAttention-2 forward with rotate-half RoPE applied to q in the kernel's Q load, gfx950");
+    m.def("rope_apply", &flash_attention::rope_apply, "rotate-half RoPE, one HIP pass (gfx950)");
     m.def("abi_version", []() { return fa_abi_version(); });
 }

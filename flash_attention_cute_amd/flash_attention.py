@@ -152,3 +152,79 @@ def flash_attn_varlen_func(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, ma
     softmax_scale = (q.size(-1) ** -0.5) if softmax_scale is None else softmax_scale
     return torch.ops.flash_attention.varlen_forward(q, k, v, cu_seqlens_q, cu_seqlens_k, int(max_seqlen_q),
                                                     int(max_seqlen_k), softmax_scale, causal)
+
+
+# ---------------------------------------------------------------------------------------------
+# RoPE: the reference rotates q and k with elementwise torch ops before the
+# call (reference models/rope_attn_fwd.py:8-38, :88). Here k is rotated in one HIP pass
+# (``apply_rope``; the KV cache stores rotated keys) and q inside the attention kernel's Q load
+# (``flash_attn_rope_func``).
+# ---------------------------------------------------------------------------------------------
+def _rope_reference(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    """x [B, H, S, D] * cos + rotate_half(x) * sin with cos / sin [B|1, S, D] or [S, D], in fp32,
+    rounded once to x's dtype (the kernels' arithmetic up to the fma)."""
+    cos = cos if cos.dim() == 3 else cos[None]
+    sin = sin if sin.dim() == 3 else sin[None]
+    xf = x.float()
+    half = x.shape[-1] // 2
+    rot = torch.cat((-xf[..., half:], xf[..., :half]), dim=-1)
+    return (xf * cos.float()[:, None] + rot * sin.float()[:, None]).to(x.dtype)
+
+
+@torch.library.custom_op("flash_attention::rope_apply", mutates_args=())
+def flash_attention_rope_apply(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    return _rope_reference(x, cos, sin)
+
+
+@torch.library.register_kernel("flash_attention::rope_apply", "cuda")
+def flash_attention_rope_apply_cuda(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    if flash_attention_cuda is None:
+        raise RuntimeError(f"gfx950 flash attention extension is not available: {_load_error!r}")
+    x = x.contiguous() if x.stride(3) != 1 else x
+    return flash_attention_cuda.rope_apply(x, cos.to(x.dtype), sin.to(x.dtype))
+
+
+@torch.library.register_fake("flash_attention::rope_apply")
+def flash_attention_rope_apply_fake(x, cos, sin):
+    return torch.empty_like(x)
+
+
+@torch.library.custom_op("flash_attention::rope_forward", mutates_args=())
+def flash_attention_rope_forward(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cos: torch.Tensor,
+                                 sin: torch.Tensor, softmax_scale: float = None, causal: bool = False) -> torch.Tensor:
+    # q unrotated [B, Hq, Sq, D]; k (already rotated), v [B, Hkv, Sk, D]; cos / sin of q's positions.
+    warnings.warn("Flash Attention only support cuda now, fallback to pytorch implementation.", stacklevel=2)
+    return torch.nn.functional.scaled_dot_product_attention(_rope_reference(q, cos, sin), k, v, scale=softmax_scale,
+                                                            is_causal=causal)
+
+
+@torch.library.register_kernel("flash_attention::rope_forward", "cuda")
+def flash_attention_rope_forward_cuda(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cos: torch.Tensor,
+                                      sin: torch.Tensor, softmax_scale: float = None,
+                                      causal: bool = False) -> torch.Tensor:
+    if flash_attention_cuda is None:
+        raise RuntimeError(f"gfx950 flash attention extension is not available: {_load_error!r}")
+    cos, sin = cos.to(q.dtype), sin.to(q.dtype)
+    if q.size(3) % 8 != 0:  # padded head dims: rotate first (the halves are those of the real D)
+        return flash_attention_forward_cuda(flash_attention_rope_apply_cuda(q, cos, sin), k, v, softmax_scale, causal)
+    q = q.contiguous() if q.stride(3) != 1 else q
+    k = k.contiguous() if k.stride(3) != 1 else k
+    v = v.contiguous() if v.stride(3) != 1 else v
+    return flash_attention_cuda.flash_attention_rope_fwd(q, k, v, cos, sin, softmax_scale, causal)
+
+
+@torch.library.register_fake("flash_attention::rope_forward")
+def flash_attention_rope_forward_fake(q, k, v, cos, sin, softmax_scale=None, causal=False):
+    return torch.empty_like(q)
+
+
+def apply_rope(x, cos, sin):
+    """Rotate-half RoPE of x [B, H, S, D] with cos / sin [B|1, S, D] or [S, D] (one HIP pass on GPU)."""
+    return torch.ops.flash_attention.rope_apply(x, cos, sin)
+
+
+def flash_attn_rope_func(q, k, v, cos, sin, softmax_scale=None, causal=False):
+    """``flash_attn_func(apply_rope(q, cos, sin), k, v, ...)`` with the rotation of q fused into the
+    attention kernel's Q load; k must already be rotated (``apply_rope``)."""
+    softmax_scale = (q.size(-1) ** -0.5) if softmax_scale is None else softmax_scale
+    return torch.ops.flash_attention.rope_forward(q, k, v, cos, sin, softmax_scale, causal)

@@ -28,7 +28,13 @@ from typing import Optional, Tuple
 import torch
 from torch import nn
 
-from .flash_attention import _bottom_right_causal, flash_attn_func, flash_attn_varlen_func
+from .flash_attention import _bottom_right_causal, apply_rope, flash_attn_func, flash_attn_rope_func, flash_attn_varlen_func
+
+# On GPU tensors the patched forward rotates k with one HIP pass (apply_rope) and q inside the
+# attention kernel (flash_attn_rope_func) instead of the reference's elementwise torch ops
+# (reference models/rope_attn_fwd.py:14-38). False restores the reference's order of operations
+# (A/B measurements, scripts/benchmark_llm.py --no-fused-rope).
+FUSE_ROPE = True
 
 
 def rotate_half(x: torch.Tensor) -> torch.Tensor:
@@ -126,10 +132,16 @@ def _flash_attention_forward(module: nn.Module, query: torch.Tensor, key: torch.
         raise NotImplementedError(
             f"flash_attention_cute_amd: sliding window {sliding_window} shorter than the {sk} visible keys")
     causal = bool(getattr(module, "is_causal", True)) and sq > 1
+    rope = kwargs.pop("rope_q", None)  # (cos, sin): q still to be rotated (fused path)
     kv_valid = key_padding(attention_mask, sq, sk, causal)
     if kv_valid is not None:
+        if rope is not None:
+            query = apply_rope(query, *rope)
         return _varlen_attention(query, key, value, kv_valid, causal, scaling), None
-    attn_output = flash_attn_func(query, key, value, causal=causal, softmax_scale=scaling)
+    if rope is not None:
+        attn_output = flash_attn_rope_func(query, key, value, *rope, causal=causal, softmax_scale=scaling)
+    else:
+        attn_output = flash_attn_func(query, key, value, causal=causal, softmax_scale=scaling)
     return attn_output.transpose(1, 2), None
 
 
@@ -151,7 +163,13 @@ def attention_forward(self: nn.Module, hidden_states: torch.Tensor,
     value_states = self.v_proj(hidden_states).view(hidden_shape).transpose(1, 2)
 
     cos, sin = position_embeddings
-    query_states, key_states = apply_rotary_pos_emb(query_states, key_states, cos, sin)
+    rope_q = None
+    if FUSE_ROPE and query_states.is_cuda:
+        # k: one HIP pass (the cache stores rotated keys); q: rotated in the attention kernel
+        key_states = apply_rope(key_states, cos, sin)
+        rope_q = (cos, sin)
+    else:
+        query_states, key_states = apply_rotary_pos_emb(query_states, key_states, cos, sin)
 
     if cache is not None:
         cache_kwargs = {"sin": sin, "cos": cos, "cache_position": cache_position}
@@ -168,7 +186,7 @@ def attention_forward(self: nn.Module, hidden_states: torch.Tensor,
     attn_output, attn_weights = _flash_attention_forward(
         self, query_states, key_states, value_states, attention_mask,
         dropout=0.0 if not self.training else self.attention_dropout, scaling=self.scaling,
-        sliding_window=sliding_window, **kwargs)
+        sliding_window=sliding_window, rope_q=rope_q, **kwargs)
 
     attn_output = attn_output.reshape(*input_shape, -1).contiguous()
     attn_output = self.o_proj(attn_output)

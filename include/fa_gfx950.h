@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define FA_GFX950_ABI_VERSION 3
+#define FA_GFX950_ABI_VERSION 4
 
 /* Field order mirrors reference csrc/flash_attention.h:5-37. */
 typedef struct fa_fwd_params {
@@ -167,6 +167,52 @@ int fa_fwd_gfx950_varlen(const fa_varlen_params *params, int dtype, int causal, 
 
 /* Host-only validation of the varlen parameters (the device arrays are not read). */
 int fa_fwd_gfx950_varlen_check(const fa_varlen_params *params, int dtype, int causal);
+
+/*
+ * RoPE fused into the attention forward (the reference applies RoPE with
+ * elementwise torch ops before the call, reference models/rope_attn_fwd.py:14-38, :88).
+ * q is given UNROTATED; the kernel rotates it (HF rotate-half convention: q * cos +
+ * rotate_half(q) * sin, fp32, one rounding to T) while loading it, with the cos / sin rows of the
+ * query positions: row of query m of batch b = b * rope_batch_stride + m * rope_seqlen_stride
+ * (elements; cos and sin share the strides, have q's dtype and head dim). k must already be rotated
+ * (fa_rope_gfx950: the KV cache stores rotated keys). Head dim 64 or 128; the prefill kernel serves
+ * every shape (no split-KV decode path). FA_ERR_UNSUPPORTED otherwise.
+ */
+typedef struct fa_rope_fwd_params {
+    fa_fwd_params base;
+    const void *rope_cos;
+    const void *rope_sin;
+    int64_t rope_batch_stride;
+    int64_t rope_seqlen_stride;
+} fa_rope_fwd_params;
+
+int fa_fwd_gfx950_rope(const fa_rope_fwd_params *params, int dtype, int causal, void *stream);
+
+/*
+ * Standalone rotate-half RoPE, out = x * cos + rotate_half(x) * sin (same arithmetic as the fused
+ * path), x / out [B, H, S, D] with element strides (out == x: in place), cos / sin rows at
+ * b * cs_batch_stride + s * cs_seqlen_stride. D even. One HBM pass; asynchronous on `stream`.
+ */
+typedef struct fa_rope_params {
+    const void *x;
+    void *out;
+    const void *cos;
+    const void *sin;
+    int64_t batch_size;
+    int64_t num_heads;
+    int64_t seqlen;
+    int64_t headdim;
+    int64_t x_batch_stride;
+    int64_t x_head_stride;
+    int64_t x_seqlen_stride;
+    int64_t out_batch_stride;
+    int64_t out_head_stride;
+    int64_t out_seqlen_stride;
+    int64_t cs_batch_stride;
+    int64_t cs_seqlen_stride;
+} fa_rope_params;
+
+int fa_rope_gfx950(const fa_rope_params *params, int dtype, void *stream);
 
 #ifdef __cplusplus
 }

@@ -229,6 +229,20 @@ def sdpa_reference_f64(q: np.ndarray, k: np.ndarray, v: np.ndarray, softmax_scal
     return out
 
 
-__all__ = ["flash_attention_fwd", "sdpa_reference_f64", "round_to", "round_bf16", "host_scale",
+def rope_rotate(x: np.ndarray, cos: np.ndarray, sin: np.ndarray, dtype: str) -> np.ndarray:
+    """Rotate-half RoPE as the gfx950 kernels compute it (csrc/fa_rope.hip, fa_fwd_kernels.hpp rope8).
+
+    Convention of the reference's caller (reference models/rope_attn_fwd.py:8-12 rotate_half,
+    :14-38 apply_rotary_pos_emb): out = x * cos + rotate_half(x) * sin, rotate_half([a, b]) = [-b, a]
+    over the last dim. Arithmetic: t = fp32(rot * sin), out = fp32(x * cos + t) (one fma), rounded
+    once (RNE) to T. x [..., S, D], cos / sin broadcastable to it, float64 arrays holding T values.
+    """
+    half = x.shape[-1] // 2
+    rot = np.concatenate([-x[..., half:], x[..., :half]], axis=-1)
+    t = round_to(rot * sin, "f32")
+    return round_to(round_to(x * cos + t, "f32"), dtype)
+
+
+__all__ = ["rope_rotate", "flash_attention_fwd", "sdpa_reference_f64", "round_to", "round_bf16", "host_scale",
            "bf16_bits_to_f64", "f64_to_bf16_bits", "fully_masked_rows", "attention_flops",
            "attention_bytes", "FLT_MAX", "LOG2E", "math"]

@@ -10,6 +10,7 @@ for dt in F16 BF16; do for c in 0 1; do for d in 64 128; do for e in 0 1; do
     -c $CS/fa_inst.hip -o $T/i_${dt}_${c}_${d}_${e}.o &
 done; done; done; done
 /opt/rocm/bin/hipcc $F -I$SRC/include -I$CS -c $CS/fa_fwd_gfx950.hip -o $T/disp.o &
+[ -f $CS/fa_rope.hip ] && /opt/rocm/bin/hipcc $F -I$SRC/include -I$CS -c $CS/fa_rope.hip -o $T/rope.o &
 wait
 mkdir -p $(dirname $OUT)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $T/*.o -o $OUT

@@ -42,7 +42,7 @@ def test_header_declares_the_boundary():
     assert set(declared_functions()) == {"fa_fwd_gfx950", "fa_fwd_gfx950_check", "fa_last_error", "fa_abi_version",
                                          "fa_fwd_gfx950_geometry", "fa_fwd_gfx950_ws",
                                          "fa_fwd_gfx950_workspace_size", "fa_fwd_gfx950_varlen",
-                                         "fa_fwd_gfx950_varlen_check"}
+                                         "fa_fwd_gfx950_varlen_check", "fa_fwd_gfx950_rope", "fa_rope_gfx950"}
 
 
 def test_every_declared_symbol_is_exported(lib):
@@ -82,7 +82,7 @@ def check(lib, p, dtype=0, causal=0):
 
 def test_abi_version(lib):
     lib.fa_abi_version.restype = ctypes.c_int
-    assert lib.fa_abi_version() == 3
+    assert lib.fa_abi_version() == 4
 
 
 def test_check_accepts_valid(lib):
