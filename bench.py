@@ -6,20 +6,25 @@ Metric (BASELINE.json): attn fwd TFLOPS + %MFMA peak at (B,H,S,D) = (4,32,4096,1
 ``flash_attn_func`` (custom op -> C++ host API -> C-ABI -> HIP kernel) over one batch of
 synthetic N(0,1) q, k, v already resident in HBM.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|decode]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|c5_layer|decode|...] [--strong]
 
-Multi-GPU (launched by torch.distributed.run, one process per GPU): every rank runs the full
-workload on its own seeded shard of batch x heads (weak scaling; attention tiles are independent,
+Multi-GPU (launched by torch.distributed.run, one process per GPU; attention tiles are independent,
 so there is no data-path collective -- SURVEY.md 8(e)). A gloo process group carries only the
 barrier and the max-over-ranks of the timings.
+  default ("weak"): every rank runs the whole configured workload on its own seeded inputs;
+  --strong        : ONE global problem (batch = --global-batch, default the config's) is split into
+                    (batch, kv-head) units by flash_attention_cute_amd/shard.py and each rank runs
+                    only its units (strided views, no copies); value = global FLOPs / slowest rank.
+c5_layer: a step is one patched ``LlamaAttention.forward`` (Llama-3-8B dims, random weights,
+reference models/rope_attn_fwd.py:66-120 with this repo's fused RoPE) -- value in tokens/s, with the
+bare op and unpatched HF (SDPA) timed beside it in the same run.
 
 Rank 0 prints ONE JSON line. Besides the contract fields it carries
   roofline     : the kernel's achieved TFLOP/s (algorithmic FLOPs / mean HIP-event duration of
                  the launches in the timed region) against the dense fp16 MFMA peak; ``traffic`` is
                  the HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/), or null;
-  cpu_baseline : the oracle/fa_oracle.c port (fp32 arithmetic, OpenMP) timed on the host cores on
-                 a bounded sample of the same workload, plus torch SDPA fp32 on the same sample
-                 (the CPU reference of BASELINE.md).
+  cpu_baseline : torch SDPA fp32 on the host cores (the reference op's CPU path, BASELINE.md's CPU
+                 baseline) on the same workload; ``port`` = oracle/fa_oracle.c on a bounded sample.
 """
 from __future__ import annotations
 
@@ -34,7 +39,7 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
-METRIC = "attn fwd TFLOPS + %MFMA peak, (B,H,S,D)=(4,32,4096,128) fp16"
+METRIC = "attn fwd TFLOPS + %MFMA peak, (B,H,S,D)=(4,32,4096,128) fp16"  # BASELINE.json (config c2)
 PEAK_TFLOPS = 2516.6  # 256 CU x 4 SIMD x 1024 FLOP/clk (32x32x16 f16/bf16 MFMA) x 2.4 GHz, dense
 HBM_PEAK_GBS = 8000.0
 
@@ -49,6 +54,10 @@ CONFIGS = {
     # over (batch, kv-head) units -- one batch row per GPU at N=8 (flash_attention_cute_amd/shard.py)
     "c5": dict(workload="C5 Llama-3-8B attn bf16 causal B1(per GPU) Hq32 Hkv8 S4096 D128", B=1, Hq=32, Hkv=8,
                Sq=4096, Sk=4096, D=128, dtype="bf16", causal=True),
+    # the patched HF attention layer around the op at C5's dims (prefill of S tokens, B per GPU)
+    "c5_layer": dict(workload="C5 layer: patched Llama-3-8B LlamaAttention.forward bf16 causal B1(per GPU) S4096 "
+                              "(hidden 4096, Hq32 Hkv8 D128, rope_theta 5e5)", B=1, Hq=32, Hkv=8, Sq=4096, Sk=4096,
+                     D=128, dtype="bf16", causal=True, hidden=4096),
     "decode": dict(workload="decode GQA fp16 B32 Hq32 Hkv8 Sq1 Sk4096 D128 (q-head pack)", B=32, Hq=32,
                    Hkv=8, Sq=1, Sk=4096, D=128, dtype="fp16", causal=False),
     # long-context decode at batch 1: the same K/V bytes as "decode" in 8 (batch, kv-head) streams,
@@ -56,6 +65,15 @@ CONFIGS = {
     "decode_long": dict(workload="decode GQA bf16 B1 Hq32 Hkv8 Sq1 Sk131072 D128 (split-KV)", B=1, Hq=32, Hkv=8,
                         Sq=1, Sk=131072, D=128, dtype="bf16", causal=False),
 }
+
+
+def metric_of(key: str, c) -> str:
+    """BASELINE.json's metric string for C2; the same metric named after the workload elsewhere."""
+    if key == "c2":
+        return METRIC
+    if key == "c5_layer":
+        return f"patched LlamaAttention.forward tokens/s, {c['workload']}"
+    return f"attn fwd TFLOPS + %MFMA peak, {c['workload']}"
 
 
 def flops(c) -> float:
@@ -78,12 +96,72 @@ def cpu_model() -> str:
 
 
 def cpu_baseline(q, k, v, c, target_s: float) -> dict:
-    """Time the oracle port and torch SDPA (fp32) on a bounded sample of batch 0's heads."""
+    """BASELINE.md's CPU baseline: torch SDPA fp32 (the reference op's own CPU implementation,
+    reference flash_attention/flash_attention.py:6-15) on the host cores, on the whole workload when
+    that fits ~20 s, else on batch 0; plus, as the "port" sub-key, oracle/fa_oracle.c (fp32,
+    OpenMP) on a bounded sample of batch 0's heads."""
     import torch
-    from oracle import fa_oracle_c as OC
 
     cores = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
     torch.set_num_threads(cores)
+    f_all = flops(c)
+    nb = c["B"] if f_all <= 20 * 1.5e12 else 1  # SDPA fp32 runs ~1.5 TFLOP/s on 16 EPYC cores
+    try:
+        qf, kf, vf = (t[:nb].float().cpu() for t in (q, k, v))
+        causal = c["causal"] and c["Sq"] > 1
+        torch.nn.functional.scaled_dot_product_attention(qf[:, :1], kf[:, :1], vf[:, :1], is_causal=causal)
+        nrep = 3
+        t0 = time.perf_counter()
+        for _ in range(nrep):
+            torch.nn.functional.scaled_dot_product_attention(qf, kf, vf, is_causal=causal, enable_gqa=True)
+        t_sdpa = (time.perf_counter() - t0) / nrep
+        f_s = flops(dict(c, B=nb))
+        out = {"value": round(f_s / t_sdpa / 1e12, 6), "unit": "TFLOPS", "cores": torch.get_num_threads(),
+               "kind": "reference",
+               "sample": f"{'the whole workload' if nb == c['B'] else 'batch 0'} of {c['workload']} "
+                         f"({f_s / 1e9:.1f} GFLOP, {t_sdpa:.3f} s per call, mean of {nrep} after 1 warm-up): "
+                         "torch SDPA fp32, the reference op's CPU path (flash_attention/flash_attention.py:6-15)",
+               "cpu_model": cpu_model()}
+        del qf, kf, vf
+    except Exception as e:  # noqa: BLE001
+        out = {"value": None, "unit": "TFLOPS", "cores": cores, "kind": "reference", "error": repr(e),
+               "cpu_model": cpu_model()}
+    out["port"] = cpu_port(q, k, v, c, target_s, cores)
+    return out
+
+
+def cpu_layer_baseline(c, seed: int) -> dict:
+    """c5_layer's CPU baseline: the unpatched HF LlamaAttention (fp32, SDPA, the reference's CPU
+    path) on the host cores, same dims, one warm-up + 2 timed calls, in tokens/s."""
+    import torch
+    from transformers import LlamaConfig
+    from transformers.models.llama import modeling_llama as ml
+
+    cores = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    torch.set_num_threads(cores)
+    cfg = LlamaConfig(hidden_size=c["hidden"], intermediate_size=14336, num_attention_heads=c["Hq"],
+                      num_key_value_heads=c["Hkv"], head_dim=c["D"], num_hidden_layers=1, vocab_size=128256,
+                      max_position_embeddings=8192, rope_theta=5e5, attn_implementation="sdpa")
+    torch.manual_seed(seed)
+    attn = ml.LlamaAttention(cfg, layer_idx=0).eval()
+    x = torch.randn(c["B"], c["Sq"], c["hidden"])
+    pe = ml.LlamaRotaryEmbedding(cfg)(x, torch.arange(c["Sq"])[None].expand(c["B"], -1))
+    with torch.no_grad():
+        attn(x, pe, None)
+        t0 = time.perf_counter()
+        for _ in range(2):
+            attn(x, pe, None)
+        t = (time.perf_counter() - t0) / 2
+    return {"value": round(c["B"] * c["Sq"] / t, 1), "unit": "tokens/s", "cores": torch.get_num_threads(),
+            "kind": "reference", "cpu_model": cpu_model(),
+            "sample": f"the whole workload ({c['B']} x {c['Sq']} tokens, {t:.2f} s per call): unpatched HF "
+                      "LlamaAttention fp32 with torch SDPA (the reference op's CPU path) on the host"}
+
+
+def cpu_port(q, k, v, c, target_s: float, cores: int) -> dict:
+    """oracle/fa_oracle.c (the CPU restatement, fp32 arithmetic, OpenMP) on a bounded sample."""
+    from oracle import fa_oracle_c as OC
+
     g = c["Hq"] // c["Hkv"]
 
     def sample(nh):
@@ -103,25 +181,9 @@ def cpu_baseline(q, k, v, c, target_s: float) -> dict:
     OC.forward(qs, ks, vs, scale, c["causal"], threads=cores)
     t_port = time.perf_counter() - t0
     f_sample = flops(dict(c, B=1, Hq=nh))
-    out = {"value": round(f_sample / t_port / 1e12, 6), "unit": "TFLOPS", "cores": cores, "kind": "port",
-           "sample": f"batch 0, q-heads 0..{nh - 1} of {c['workload']} ({f_sample / 1e9:.1f} GFLOP, "
-                     f"{t_port:.2f} s, oracle/fa_oracle.c fp32 OpenMP)",
-           "cpu_model": cpu_model()}
-    # torch SDPA fp32 on the same sample (BASELINE.md's CPU reference): 1 warm-up + 3 reps
-    try:
-        qf, kf, vf = (t.float() for t in (qs, ks, vs))
-        nrep = 3
-        torch.nn.functional.scaled_dot_product_attention(qf[:, :1], kf[:, :1], vf[:, :1], is_causal=c["causal"])
-        t0 = time.perf_counter()
-        for _ in range(nrep):
-            torch.nn.functional.scaled_dot_product_attention(qf, kf, vf, is_causal=c["causal"] and c["Sq"] > 1,
-                                                             enable_gqa=True)
-        t_sdpa = (time.perf_counter() - t0) / nrep
-        out["sdpa_fp32"] = {"value": round(f_sample / t_sdpa / 1e12, 6), "unit": "TFLOPS",
-                            "threads": torch.get_num_threads(), "seconds": round(t_sdpa, 3)}
-    except Exception as e:  # noqa: BLE001
-        out["sdpa_fp32"] = {"error": repr(e)}
-    return out
+    return {"value": round(f_sample / t_port / 1e12, 6), "unit": "TFLOPS", "cores": cores, "kind": "port",
+            "sample": f"batch 0, q-heads 0..{nh - 1} of {c['workload']} ({f_sample / 1e9:.1f} GFLOP, "
+                      f"{t_port:.2f} s, oracle/fa_oracle.c fp32 OpenMP)"}
 
 
 def load_traffic(config_key: str):
@@ -134,18 +196,63 @@ def load_traffic(config_key: str):
         return None
 
 
-def roofline(c, kern_ms: float, traffic):
+def roofline(c, kern_ms: float, traffic, rank_flops=None, rank_bytes=None):
     """Roofline of the attention kernel: MFMA-bound for prefill (intensity ~2 kFLOP/B at S=4096),
-    HBM-bound for decode (Sq = 1: one pass over K/V per q-head group)."""
-    gbs = algo_bytes(c) / (kern_ms * 1e-3) / 1e9
-    tf = flops(c) / (kern_ms * 1e-3) / 1e12
-    base = {"traffic": traffic, "kernel_ms": round(kern_ms, 4), "algorithmic_bytes": algo_bytes(c),
-            "algorithmic_flops": flops(c)}
+    HBM-bound for decode (Sq = 1: one pass over K/V per q-head group). ``rank_*``: the work of the
+    launches timed (one rank's shard under --strong), default the whole config."""
+    fl = flops(c) if rank_flops is None else rank_flops
+    by = algo_bytes(c) if rank_bytes is None else rank_bytes
+    gbs = by / (kern_ms * 1e-3) / 1e9
+    tf = fl / (kern_ms * 1e-3) / 1e12
+    base = {"traffic": traffic, "kernel_ms": round(kern_ms, 4), "algorithmic_bytes": by,
+            "algorithmic_flops": fl}
     if c["Sq"] == 1:
         return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gbs / HBM_PEAK_GBS, 4), "achieved_TFLOPs": round(tf, 3), **base}
     return {"bound": "mfma", "achieved": round(tf, 3), "peak": PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tf / PEAK_TFLOPS, 4), "algorithmic_GBs": round(gbs, 1), **base}
+
+
+def layer_setup(c, dev, dt, seed):
+    """C5's caller: one Llama-3-8B attention layer (random weights; transformers' LlamaAttention with
+    its forward patched to flash_attention_cute_amd.hf_attention.attention_forward, as reference
+    models/patch_llama.py:4-5 does) over B x S tokens of prefill. Returns the patched step and, for
+    timing beside it, the unpatched HF (SDPA) layer and the patched layer with the reference's
+    unfused torch RoPE."""
+    import torch
+    from transformers import LlamaConfig
+    from transformers.models.llama import modeling_llama as ml
+
+    from flash_attention_cute_amd import hf_attention
+
+    cfg = LlamaConfig(hidden_size=c["hidden"], intermediate_size=14336, num_attention_heads=c["Hq"],
+                      num_key_value_heads=c["Hkv"], head_dim=c["D"], num_hidden_layers=1, vocab_size=128256,
+                      max_position_embeddings=8192, rope_theta=5e5, attn_implementation="sdpa")
+    torch.manual_seed(seed)
+    attn = ml.LlamaAttention(cfg, layer_idx=0).to(dev, dt).eval()
+    rope = ml.LlamaRotaryEmbedding(cfg).to(dev)
+    x = torch.randn(c["B"], c["Sq"], c["hidden"], device=dev, dtype=dt)
+    pe = rope(x, torch.arange(c["Sq"], device=dev)[None].expand(c["B"], -1))
+    orig = ml.LlamaAttention.forward
+
+    def patched_call():
+        with torch.no_grad():
+            return hf_attention.attention_forward(attn, x, pe, None)[0]
+
+    def hf_call():
+        with torch.no_grad():
+            return orig(attn, x, pe, None)[0]
+
+    def unfused_call():
+        hf_attention.FUSE_ROPE = False
+        try:
+            return patched_call()
+        finally:
+            hf_attention.FUSE_ROPE = True
+
+    proj = 2.0 * c["B"] * c["Sq"] * c["hidden"] * (2 * c["Hq"] * c["D"] + 2 * c["Hkv"] * c["D"])
+    info = {"projection_flops": proj, "attention_flops": flops(c), "_hf_step": hf_call, "_unfused_step": unfused_call}
+    return patched_call, info
 
 
 def reduce_max(world: int, *vals: float):
@@ -166,9 +273,11 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
+    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="CPU port sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--strong", action="store_true", help="split one global problem over the ranks (shard.py)")
+    ap.add_argument("--global-batch", type=int, default=0, help="--strong: global batch (default: the config's)")
     ap.add_argument("--warmup-seconds", type=float, default=2.0,
                     help="back-to-back op calls before the W warm-up steps (the clock settles)")
     args = ap.parse_args()
@@ -201,14 +310,56 @@ def main() -> None:
 
     c = CONFIGS[args.config]
     dt = torch.float16 if c["dtype"] == "fp16" else torch.bfloat16
-    gen = torch.Generator(device=dev).manual_seed(args.seed + rank)  # per-rank shard of batch x heads
-    q = torch.randn(c["B"], c["Hq"], c["Sq"], c["D"], device=dev, dtype=dt, generator=gen)
-    k = torch.randn(c["B"], c["Hkv"], c["Sk"], c["D"], device=dev, dtype=dt, generator=gen)
-    v = torch.randn(c["B"], c["Hkv"], c["Sk"], c["D"], device=dev, dtype=dt, generator=gen)
+    layer = args.config == "c5_layer"
+    extra = {}
+    if args.strong:
+        # one global problem, this rank's (batch, kv-head) units (shard.py); same seed on every rank
+        from flash_attention_cute_amd import shard
 
-    def step():
-        return flash_attn_func(q, k, v, causal=c["causal"])
+        gb = args.global_batch or c["B"]
+        c = dict(c, B=gb, workload=f"{c['workload']} -> global batch {gb} split over {world} GPU(s)")
+        gen = torch.Generator(device=dev).manual_seed(args.seed)
+        q = torch.randn(gb, c["Hq"], c["Sq"], c["D"], device=dev, dtype=dt, generator=gen)
+        k = torch.randn(gb, c["Hkv"], c["Sk"], c["D"], device=dev, dtype=dt, generator=gen)
+        v = torch.randn(gb, c["Hkv"], c["Sk"], c["D"], device=dev, dtype=dt, generator=gen)
+        runs = shard.rank_runs(gb, c["Hkv"], world, rank)
+        g = c["Hq"] // c["Hkv"]
+        views = [(q[r.b:r.b_end, r.h0 * g:r.h1 * g], k[r.b:r.b_end, r.h0:r.h1], v[r.b:r.b_end, r.h0:r.h1])
+                 for r in runs]
+        rank_flops = sum(flops(dict(c, B=r.b_end - r.b, Hq=(r.h1 - r.h0) * g)) for r in runs)
+        rank_bytes = sum(algo_bytes(dict(c, B=r.b_end - r.b, Hq=(r.h1 - r.h0) * g, Hkv=r.h1 - r.h0)) for r in runs)
 
+        def step():
+            return [flash_attn_func(a, b_, v_, causal=c["causal"]) for a, b_, v_ in views]
+
+        extra["shard"] = {"units": f"{c['B'] * c['Hkv']} (batch, kv-head)", "rank0_runs": len(runs)}
+    else:
+        gen = torch.Generator(device=dev).manual_seed(args.seed + rank)  # per-rank shard of batch x heads
+        q = torch.randn(c["B"], c["Hq"], c["Sq"], c["D"], device=dev, dtype=dt, generator=gen)
+        k = torch.randn(c["B"], c["Hkv"], c["Sk"], c["D"], device=dev, dtype=dt, generator=gen)
+        v = torch.randn(c["B"], c["Hkv"], c["Sk"], c["D"], device=dev, dtype=dt, generator=gen)
+        rank_flops, rank_bytes = flops(c), algo_bytes(c)
+
+        def step():
+            return flash_attn_func(q, k, v, causal=c["causal"])
+
+    if layer:
+        layer_step, layer_info = layer_setup(c, dev, dt, args.seed + rank)
+        extra["layer"] = layer_info
+
+    def timed(fn, n):
+        """n calls of fn between synchronisations: (wall s, mean HIP-event ms per call)."""
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(n):
+            ev[i][0].record()
+            fn()
+            ev[i][1].record()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, sum(a.elapsed_time(b) for a, b in ev) / n
+
+    main_step = layer_step if layer else step
     # Device warm-up: the MI355X ramps its clock over the first ~second of sustained load, so a
     # few warm-up steps leave the timed steps on a still-rising clock (C2: 1043 TFLOPS after 5
     # warm-up steps vs 1099 after 1000, same binary and box). Run the same op back to back for
@@ -216,54 +367,74 @@ def main() -> None:
     t_w = time.perf_counter()
     while time.perf_counter() - t_w < args.warmup_seconds:
         for _ in range(10):
-            step()
+            main_step()
         torch.cuda.synchronize()
     for _ in range(args.warmup):
-        step()
+        main_step()
     torch.cuda.synchronize()
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if layer:  # the bare op and unpatched HF at the same dims, timed beside the patched layer
+        for key, fn in (("bare_op_ms", step), ("hf_sdpa_layer_ms", layer_info.pop("_hf_step")),
+                        ("unfused_rope_layer_ms", layer_info.pop("_unfused_step"))):
+            timed(fn, 10)  # warm-up (library heuristics, first-call setup)
+            extra["layer"][key] = round(timed(fn, max(args.steps, 10))[1], 4)
+        for _ in range(args.warmup):
+            main_step()
+
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record()
-        step()
-        ev[i][1].record()
-    torch.cuda.synchronize()
+    elapsed, step_ms = timed(main_step, args.steps)
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    # the attention kernel alone (roofline): HIP events around the op's launches on the current stream
+    kern_ms = step_ms if not layer else extra["layer"]["bare_op_ms"]
 
-    elapsed, kern_ms = reduce_max(world, elapsed, kern_ms)
+    (elapsed,) = reduce_max(world, elapsed)
 
-    f_step = flops(c)
-    value = n_gpus * f_step * args.steps / elapsed / 1e12
+    if layer:
+        tokens = n_gpus * c["B"] * c["Sq"] * args.steps
+        value, unit = tokens / elapsed, "tokens/s"
+        extra["layer"]["layer_ms"] = round(elapsed * 1e3 / args.steps, 4)
+        extra["layer"]["hf_sdpa_tokens_per_s"] = round(c["B"] * c["Sq"] / (extra["layer"]["hf_sdpa_layer_ms"] * 1e-3), 1)
+        extra["layer"]["layer_TFLOPS"] = round((extra["layer"]["projection_flops"] + extra["layer"]["attention_flops"])
+                                               / (elapsed / args.steps) / 1e12, 2)
+    elif args.strong:
+        value, unit = flops(c) * args.steps / elapsed / 1e12, "TFLOPS"
+    else:
+        value, unit = n_gpus * flops(c) * args.steps / elapsed / 1e12, "TFLOPS"
+    tf_per_gpu = (flops(c) / n_gpus if args.strong else flops(c)) * args.steps / elapsed / 1e12
     result = {
-        "metric": METRIC,
+        "metric": metric_of(args.config, c),
         "value": round(value, 3),
-        "unit": "TFLOPS",
+        "unit": unit,
         "n_gpus": n_gpus,
         "steps": args.steps,
         "warmup": args.warmup,
         "device_warmup_s": args.warmup_seconds,
         "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": c["dtype"],
-        "data": "synthetic N(0,1) q/k/v, seed + rank, resident in HBM",
+        "data": ("synthetic N(0,1) q/k/v, one global seed, sharded by (batch, kv-head)" if args.strong else
+                 "synthetic N(0,1) q/k/v, seed + rank, resident in HBM") +
+                ("; random-init Llama-3-8B attention weights, no checkpoint" if layer else ""),
         "config": {"workload": c["workload"], "batch": c["B"], "heads_q": c["Hq"], "heads_kv": c["Hkv"],
                    "seqlen_q": c["Sq"], "seqlen_kv": c["Sk"], "headdim": c["D"], "causal": c["causal"],
-                   "parallelism": f"dp{n_gpus} (independent batch x head shard per GPU, no collective)"},
-        "pct_mfma_peak": round(100.0 * value / n_gpus / PEAK_TFLOPS, 2),
-        "roofline": roofline(c, kern_ms, load_traffic(args.config)),
+                   "parallelism": (f"dp{n_gpus}: (batch, kv-head) units of one problem split over ranks, no collective"
+                                   if args.strong else
+                                   f"dp{n_gpus} (independent batch x head shard per GPU, no collective)")},
+        "pct_mfma_peak": None if layer else round(100.0 * tf_per_gpu / PEAK_TFLOPS, 2),
+        # rank 0's kernel: its FLOPs / bytes over the mean HIP-event time of its launches
+        "roofline": roofline(c, kern_ms, load_traffic(args.config) if not args.strong else None,
+                             rank_flops=rank_flops, rank_bytes=rank_bytes),
         "cpu_baseline": None,
+        **extra,
     }
     if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(q, k, v, c, args.cpu_seconds)
+        result["cpu_baseline"] = (cpu_layer_baseline(c, args.seed) if layer else
+                                  cpu_baseline(q, k, v, c, args.cpu_seconds))
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -8,8 +8,9 @@ crosses devices and each rank streams only the K/V it owns. One process per GPU;
 cross-rank traffic is the harness's barrier and max-of-timings (bench.py), never tensor data.
 
 ``plan(B, Hkv, world)`` splits the B*Hkv units into ``world`` contiguous, balanced ranges;
-``rank_runs(...)`` turns one rank's range into per-batch runs of consecutive kv-heads, each of
-which is ONE call of the op on strided views (no copies); ``sharded_forward`` runs them.
+``rank_runs(...)`` turns one rank's range into runs -- whole batch rows merged into one, partial rows
+as consecutive kv-heads -- each of which is ONE call of the op on strided views (no copies);
+``sharded_forward`` runs them.
 """
 from __future__ import annotations
 
@@ -19,11 +20,17 @@ from typing import Callable, List, Tuple
 
 @dataclass(frozen=True)
 class Run:
-    """Batch ``b``, kv-heads ``[h0, h1)`` (q-heads ``[h0*g, h1*g)``)."""
+    """Batch rows ``[b, b1)`` x kv-heads ``[h0, h1)`` (q-heads ``[h0*g, h1*g)``): one op call. A run
+    spans several batch rows only when it covers all their kv-heads (``b1`` defaults to ``b + 1``)."""
 
     b: int
     h0: int
     h1: int
+    b1: int = -1
+
+    @property
+    def b_end(self) -> int:
+        return self.b + 1 if self.b1 < 0 else self.b1
 
 
 def plan(batch: int, heads_kv: int, world: int) -> List[Tuple[int, int]]:
@@ -49,6 +56,11 @@ def rank_runs(batch: int, heads_kv: int, world: int, rank: int) -> List[Run]:
     u = s
     while u < e:
         b, h = divmod(u, heads_kv)
+        if h == 0 and e - u >= heads_kv:  # whole batch rows: one call over [b, b + n)
+            n = (e - u) // heads_kv
+            runs.append(Run(b, 0, heads_kv, b + n))
+            u += n * heads_kv
+            continue
         h1 = min(heads_kv, h + (e - u))
         runs.append(Run(b, h, h1))
         u += h1 - h
@@ -68,9 +80,9 @@ def sharded_forward(q, k, v, rank: int, world: int, fn: Callable, **kw):
     g = Hq // Hkv
     res = []
     for run in rank_runs(B, Hkv, world, rank):
-        qs = q[run.b:run.b + 1, run.h0 * g:run.h1 * g]
-        ks = k[run.b:run.b + 1, run.h0:run.h1]
-        vs = v[run.b:run.b + 1, run.h0:run.h1]
+        qs = q[run.b:run.b_end, run.h0 * g:run.h1 * g]
+        ks = k[run.b:run.b_end, run.h0:run.h1]
+        vs = v[run.b:run.b_end, run.h0:run.h1]
         res.append((run, fn(qs, ks, vs, **kw)))
     return res
 
@@ -79,5 +91,5 @@ def assemble(shards, out):
     """Write [(Run, out)] from ``sharded_forward`` into the global output ``out`` [B, Hq, Sq, D]."""
     for run, o in shards:
         g = o.shape[1] // (run.h1 - run.h0)
-        out[run.b:run.b + 1, run.h0 * g:run.h1 * g] = o
+        out[run.b:run.b_end, run.h0 * g:run.h1 * g] = o
     return out

@@ -24,9 +24,12 @@ def test_plan_is_a_balanced_partition(B, H, W):
     assert max(sizes) - min(sizes) <= 1
     seen = []
     for r in range(W):
-        for run in shard.rank_runs(B, H, W, r):
-            assert 0 <= run.b < B and 0 <= run.h0 < run.h1 <= H
-            seen += [(run.b, h) for h in range(run.h0, run.h1)]
+        runs = shard.rank_runs(B, H, W, r)
+        for run in runs:
+            assert 0 <= run.b < run.b_end <= B and 0 <= run.h0 < run.h1 <= H
+            assert run.b_end == run.b + 1 or (run.h0, run.h1) == (0, H)  # multi-row runs are whole rows
+            seen += [(b, h) for b in range(run.b, run.b_end) for h in range(run.h0, run.h1)]
+        assert len(runs) <= 3  # a partial row, whole rows in one call, a partial row
     assert sorted(seen) == [(b, h) for b in range(B) for h in range(H)]
 
 
@@ -64,7 +67,7 @@ def _worker(rank, world, port, case, ret):
         out = shard.assemble(parts, torch.zeros(B, Hq, Sq, D, dtype=torch.float32))
         cover = torch.zeros(B, Hq)
         for run, _ in parts:
-            cover[run.b, run.h0 * (Hq // Hkv):run.h1 * (Hq // Hkv)] = 1
+            cover[run.b:run.b_end, run.h0 * (Hq // Hkv):run.h1 * (Hq // Hkv)] = 1
         dist.all_reduce(out)
         dist.all_reduce(cover)
         if rank == 0:
