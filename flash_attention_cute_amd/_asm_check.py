@@ -4,7 +4,7 @@
 inline asm reads and writes (csrc/fa_agpr_asm.inc). The compiler does not know these registers are
 live across the separate asm statements, so a compiler-generated AGPR use in that range (for example
 a VGPR spill to an AGPR after a toolchain or code change) would silently corrupt the output. This
-module scans the ``-save-temps`` assembly: any use of a0..a191 outside ``;;#ASMSTART``/``;;#ASMEND``
+module scans the ``-save-temps`` assembly: any use of those AGPRs (a0..a63 at D = 64) outside ``;;#ASMSTART``/``;;#ASMEND``
 inside ``fa_fwd_w4``, or any kernel with ``.vgpr_spill_count`` > 0, fails the build.
 
 CLI: ``python -m flash_attention_cute_amd._asm_check file.s [...]``
@@ -14,8 +14,17 @@ from __future__ import annotations
 import re
 import sys
 
-PINNED = 192  # a0..a127 (O) and a128..a191 (Q) belong to the inline asm (fa_agpr_asm.inc)
+QBASE, QEND = 128, 192  # the Q fragments a128..a191 belong to the inline asm (fa_agpr_asm.inc)
 _REG = re.compile(r"\ba\[(\d+)(?::\d+)?\]|\ba(\d+)\b")
+_TILE = re.compile(r"ELi(64|128)ELb")  # the head-dim tile template argument of the mangled name
+
+
+def pinned(fn: str, reg: int) -> bool:
+    """a0..a(head-dim tile - 1) hold O^T of both 32-row blocks (D/32 d-tiles x 16 each x 2 blocks),
+    a128..a191 the Q fragments; at D = 64 the compiler may use a64..a127."""
+    m = _TILE.search(fn)
+    o_end = int(m.group(1)) if m else 128
+    return reg < o_end or QBASE <= reg < QEND
 
 
 def agpr_violations(text: str) -> list[str]:
@@ -32,7 +41,7 @@ def agpr_violations(text: str) -> list[str]:
             in_asm = False
         elif fn and not in_asm and not ln.lstrip().startswith(";"):
             for r in _REG.finditer(ln.split(";")[0]):
-                if int(r.group(1) or r.group(2)) < PINNED:
+                if pinned(fn, int(r.group(1) or r.group(2))):
                     bad.append(f"{fn}: {ln.strip()}")
                     break
     return bad

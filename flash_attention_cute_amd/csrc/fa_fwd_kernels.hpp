@@ -205,6 +205,16 @@ __device__ __forceinline__ rsrc_t make_rsrc(const char *base, uint32_t nbytes) {
     return __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)nbytes, 0x00020000);
 }
 
+// the same from values the compiler cannot prove wave-uniform (loaded from memory, carried across
+// branches): readfirstlane keeps the descriptor in SGPRs (the values are uniform by construction)
+__device__ __forceinline__ rsrc_t make_rsrc_u(const char *base, uint32_t nbytes) {
+    const uint64_t a = (uint64_t)(uintptr_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const char *ub = (const char *)(uintptr_t)(((uint64_t)hi << 32) | lo);
+    return make_rsrc(ub, __builtin_amdgcn_readfirstlane(nbytes));
+}
+
 // bytes of the first `rows` (<= 64) rows of a [rows, D] slab with row stride `stride` elements;
 // 0 if rows <= 0. The host guarantees 64 * stride * 2 + 256 < 2^31.
 __device__ __forceinline__ uint32_t slab_bytes(int rows, int stride, int D) {
@@ -626,6 +636,15 @@ __device__ __forceinline__ void agpr_qload(const rsrc_t &rs, const int voff, con
     FA_CASE(160) FA_CASE(164) FA_CASE(168) FA_CASE(172) FA_CASE(176) FA_CASE(180) FA_CASE(184) FA_CASE(188)
 #undef FA_CASE
 }
+// one Q fragment from LDS (staged there by LDS-DMA) straight into a[QB .. QB+3]
+template <int QB>
+__device__ __forceinline__ void agpr_qlds(const uint32_t addr) {
+#define FA_CASE(N) \
+    if constexpr (QB == N) fa_agpr_qlds_##N(addr);
+    FA_CASE(128) FA_CASE(132) FA_CASE(136) FA_CASE(140) FA_CASE(144) FA_CASE(148) FA_CASE(152) FA_CASE(156)
+    FA_CASE(160) FA_CASE(164) FA_CASE(168) FA_CASE(172) FA_CASE(176) FA_CASE(180) FA_CASE(184) FA_CASE(188)
+#undef FA_CASE
+}
 // first k-step with C = bias (the running reference max, kFoldScale)
 template <bool kF16, int QB>
 __device__ __forceinline__ void mfma_sq_bias(f32x16 &acc, const u32x4 &a, const f32x16 &bias) {
@@ -773,10 +792,25 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     static_assert(kV0 >= 4 && kV0 < 32 && kV0 % 2 == 0, "kV0");
     constexpr int kNL = 2 * (32 - kV0);  // late exp units of phase 1
     constexpr int QB = 128;  // Q fragments: AGPRs a[QB + 4*(X*KS + ks)] (fa_agpr_asm.inc)
+#ifndef FA_QLDS
+#define FA_QLDS 2
+#endif
+    // Q staging (kQL): 0 = HBM -> AGPR loads issued under the previous block's drain; 1 = LDS-DMA
+    // into a Q image (K's swizzle) under the drain, read into the AGPRs at the block prologue;
+    // 2 = the same pieces spread over the previous block's tiles (kQPT per tile, phase 1), so the
+    // block switch moves no Q bytes
+    constexpr int kQL = FA_QLDS;
+    constexpr int kQPT = 2;
+#ifndef FA_QPH
+#define FA_QPH 2
+#endif
+    constexpr int kQPhase = FA_QPH;  // phase of the tile that issues them
+    constexpr int NQP = T / 1024;  // Q pieces per wave (its 64 rows): 16 / 8
     // LDS: K slots 0,1 | V slots 0,1 (64 KiB at D = 128), so every fragment read is a per-lane base
-    // plus a 16-bit immediate offset. Q is read once from HBM straight into AGPRs.
+    // plus a 16-bit immediate offset; then (kQL) the Q image, T bytes per wave.
     constexpr int KV0 = 0;
-    __shared__ __attribute__((aligned(1024))) char lds[4 * T];
+    constexpr int QOFF = 4 * T;
+    __shared__ __attribute__((aligned(1024))) char lds[(kQL ? 8 : 4) * T];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -812,8 +846,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     const char *cosb = nullptr, *sinb = nullptr;  // RoPE tables of this block's sequence (rope.cos)
     char *ob;
     int m0, mw, n_end, n_pipe;
-    auto set_block = [&](const uint32_t k) {
-        const Work wk = decode_work<kCausal>(nwg, xcd + 8 * k, n_qtiles, (int)p.num_heads_q);
+    auto set_block = [&](const Work wk) {
         const int hq = wk.hq, b = wk.b;
         const int hkv = hq / (int)p.head_q_per_group;
         int64_t qrow0 = (int64_t)b * p.q_batch_stride, krow0 = (int64_t)b * p.k_batch_stride;
@@ -856,7 +889,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         }
         n_pipe = min(n_pipe, n_end);
     };
-    set_block(kblk);
+    set_block(decode_work<kCausal>(nwg, xcd + 8 * kblk, n_qtiles, (int)p.num_heads_q));
 
     // ---- Q: this wave's 64 rows, B-operand fragments straight from HBM into AGPRs ----------
     // lane (h, r) of block X holds Q[mw + 32X + r][16*ks + 8*h + 0..7]; rows >= Sq read as 0.
@@ -910,7 +943,59 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             });
         });
     };
-    if (!rope_q) load_q();
+    // ---- Q by LDS-DMA (kQL): piece n (0..NQP-1) holds rows n*RPP.. of this wave's 64 in K's
+    // swizzled image. Lane l writes image bytes n*1024 + 16 l = row n*RPP + 16 l / RB, slot
+    // (16 l % RB) / 16; its source chunk is the slot XOR the row term of Geo::k_off, which for piece
+    // n is the lane's piece-0 term XOR 4 * (n mod 4) (D = 128) or 4 * (n mod 2) (D = 64).
+    const int qs_ = (int)p.q_seqlen_stride;
+    const int q_row_l = (16 * lane) / RB;
+    const int q_ch0 = G::k_off(q_row_l, ((16 * lane) % RB) / 16) % RB / 16;
+    const uint32_t q_lane_off = (uint32_t)(q_row_l * qs_ * 2);
+    const uint32_t q_lds = lds_u32(lds) + QOFF + wave * T;  // this wave's Q image
+    auto q_piece = [&](const rsrc_t &qr, const int n) __attribute__((always_inline)) {
+        const int ch = q_ch0 ^ (4 * (n & (RB == 256 ? 3 : 1)));
+        uint32_t voff = q_lane_off + (uint32_t)(n * ROWS_PER_PIECE * qs_ * 2) + 16u * (uint32_t)ch;
+        if (!kExactD && ch * 8 >= D) voff = 0x7ffffff0u;  // columns past D read as 0
+        dma_one(qr, q_lds + n * 1024, (int)voff, true);
+    };
+    // this wave's Q slab of block wk (rows past the sequence read as 0)
+    auto q_rsrc_of = [&](const Work wk) __attribute__((always_inline)) {
+        int64_t row0 = (int64_t)wk.b * p.q_batch_stride;
+        int sq = (int)p.seqlen_q;
+        if (cu_q) {
+            const int q0 = cu_q[wk.b];
+            sq = cu_q[wk.b + 1] - q0;
+            row0 = (int64_t)q0 * qs_;
+        }
+        const int mwn = wk.qtile * kBlockM + wave * 64;
+        const char *qbn = (const char *)p.q_ptr + 2 * (row0 + (int64_t)wk.hq * p.q_head_stride);
+        return make_rsrc_u(qbn + 2 * (int64_t)mwn * qs_, slab_bytes(min(sq - mwn, 64), qs_, D));
+    };
+    // the next block (decoded once, in this block's prologue) and its Q pieces: qn of qnt issued
+    // (kQL == 2: during this block's tiles)
+    Work wk_next = {0, 0, 0};
+    rsrc_t qnr = make_rsrc(nullptr, 0u);
+    int qn = 0, qnt = 0;
+    auto plan_next = [&]() __attribute__((always_inline)) {
+        const uint32_t kn = block_of(rnd + 1);
+        qn = 0;
+        qnt = 0;
+        if (kn < cnt) {
+            wk_next = decode_work<kCausal>(nwg, xcd + 8 * kn, n_qtiles, (int)p.num_heads_q);
+            if (kQL && !rope_q) {
+                qnr = q_rsrc_of(wk_next);
+                qnt = NQP;
+            }
+        }
+    };
+    if (!rope_q) {
+        if constexpr (kQL != 0) {
+            const rsrc_t qr0 = q_rsrc_of(decode_work<kCausal>(nwg, xcd + 8 * kblk, n_qtiles, (int)p.num_heads_q));
+            static_for<NQP>([&](auto N) { q_piece(qr0, decltype(N)::value); });
+        } else {
+            load_q();
+        }
+    }
 
     // ---- LDS-DMA staging: this wave writes pieces (wave*NP + n) of each K and V tile --------
     const int ks_ = (int)p.k_seqlen_stride, vs_ = (int)p.v_seqlen_stride;
@@ -946,6 +1031,16 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     int k_addr[KS];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) k_addr[ks] = G::k_off(r, 2 * ks + h);
+    // a block's Q image -> the Q AGPRs (its pieces have landed: the caller waited vmcnt; the
+    // caller also waits lgkmcnt before the first S MFMA). The B-operand fragment (block X, k-step
+    // ks) sits where K's A-operand fragment does, 32X rows on.
+    auto q_from_lds = [&]() __attribute__((always_inline)) {
+        static_for<2 * KS>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            agpr_qlds<QB + 4 * i>(q_lds + (i / KS) * 32 * RB + k_addr[i % KS]);
+        });
+    };
+    bool q_in_agpr = false;  // the block's Q was read into the AGPRs at the switch
     // ---- state ------------------------------------------------------------------------------
     struct Sm {               // online-softmax state of one block (per lane: one query row)
         float m, msc, alpha;  // running max (unscaled), m*sc, alpha of the last decision
@@ -1108,6 +1203,13 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                 if constexpr (ks < NP) dma_one_at<pr * T + ks * 1024>(kr, lds_base, kvo[ks], ks == 0);
                 else dma_one_at<(2 + c) * T + (ks - NP) * 1024>(vr, lds_base, vvo[ks - NP], ks == NP);
             }
+            // the next block's Q: kQPT pieces per tile, in evenly spaced gaps
+            if constexpr (kQL == 2 && kQPhase == 1 && do_dma && i == 3 && (ks * kQPT) % KS == 0) {
+                if (qn < qnt) {
+                    q_piece(qnr, qn);
+                    ++qn;
+                }
+            }
             if constexpr (do_sm) {
                 static_for<kNL>([&](auto U) {
                     constexpr int u = decltype(U)::value;
@@ -1199,6 +1301,13 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             if constexpr (kk + 1 < 4 && i < DTL) {
                 rd(kk + 1, 2 * i, va[(kk + 1) & 1]);
                 rd(kk + 1, 2 * i + 1, va[(kk + 1) & 1]);
+            }
+            // (kQPhase 2) the next block's Q pieces early in phase 2, where no K/V DMA is issued
+            if constexpr (kQL == 2 && kQPhase == 2 && do_sm && g % 2 == 1 && g < 2 * kQPT) {
+                if (qn < qnt) {
+                    q_piece(qnr, qn);
+                    ++qn;
+                }
             }
             if constexpr (do_sm) {
                 static_for<32>([&](auto M) {
@@ -1294,6 +1403,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // Q, K_0 landed. After the first block the previous block's O stores were issued after these
     // loads: leave them in flight (vmcnt counts stores too, in issue order)
     if (rnd == 0) dma_wait(); else __builtin_amdgcn_s_waitcnt(vmcnt_enc(kOStores));
+    if (kQL && !rope_q && !q_in_agpr) q_from_lds();
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
+    plan_next();
     __syncthreads();  // visible to every wave
     FA_STAMP(s_pro);
 
@@ -1406,9 +1518,18 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     kblk = block_of(++rnd);
     const bool more = kblk < cnt;
     if (more) {
-        set_block(kblk);
-        if (!rope_q) load_q();
+        set_block(wk_next);
+        // kQL: when this block's tiles issued all the next block's Q pieces they have landed (each
+        // tile waits vmcnt(0)), so Q goes into the AGPRs now, under the drain; else the rest is
+        // issued here and read in the prologue
+        q_in_agpr = kQL && qnt > 0 && qn == qnt;
+        if constexpr (kQL != 0) {
+            for (; qn < qnt; ++qn) q_piece(qnr, qn);
+        } else if (!rope_q) {
+            load_q();
+        }
         stage_k(0);
+        if (q_in_agpr) q_from_lds();
     }
     // drain the last pipelined tile: softmax half 2 and P.V
     auto drain = [&](auto PAR) __attribute__((always_inline)) {

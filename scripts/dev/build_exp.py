@@ -4,7 +4,7 @@ import sys
 from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 from flash_attention_cute_amd import _build  # noqa: E402
 
 ONLY = (("F16", 0, 128, 1), ("F16", 1, 128, 1), ("BF16", 1, 128, 1))

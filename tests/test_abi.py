@@ -222,6 +222,11 @@ def test_asm_check_detects_pinned_agpr_use_and_spills():
     assert len(A.agpr_violations(bad)) == 1
     other = bad.replace("fa_fwd_w4", "fa_decode")  # only fa_fwd_w4 pins AGPRs
     assert A.agpr_violations(other) == []
+    # the head-dim tile sets the O range: a64..a127 are free at D = 64, pinned at D = 128
+    d64 = ok.replace("IXEE", "INS_3F16ELb0ELi64ELb1EE").replace("a200", "a70")
+    assert A.agpr_violations(d64) == []
+    assert len(A.agpr_violations(d64.replace("Li64E", "Li128E"))) == 1
+    assert len(A.agpr_violations(d64.replace("a70", "a130"))) == 1  # Q: pinned at every D
     meta = "amdhsa.kernels:\n  - .agpr_count: 0\n    .name: k1\n    .vgpr_spill_count: 0\n" \
            "  - .agpr_count: 0\n    .name: k2\n    .vgpr_spill_count: 3\n"
     assert A.spills(meta) == ["k2: vgpr_spill_count 3"]
