@@ -1149,11 +1149,15 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             P[c][4 * X + 2 * hf + (v >> 3)][(v & 7) >> 1] = w;
         }
     };
-    auto rescale = [&]() {
+    // o_zero: O holds no P.V yet (a block's first tile, where every row takes its first reference):
+    // scaling it is a no-op, so only l is updated
+    auto rescale = [&](const bool o_zero) {
         // rare: one branch for both blocks (a block that did not rescale has alpha = 1)
         if (__builtin_expect((st[0].rmask | st[1].rmask) != 0, 0)) {
-            agpr_scale<DTL, false>(st[0].alpha);
-            agpr_scale<DTL, true>(st[1].alpha);
+            if (!o_zero) {
+                agpr_scale<DTL, false>(st[0].alpha);
+                agpr_scale<DTL, true>(st[1].alpha);
+            }
 #pragma unroll
             for (int X = 0; X < 2; ++X) {
                 st[X].l = __builtin_fmaf(st[X].l, st[X].alpha, st[X].t);
@@ -1448,7 +1452,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #else
         phase2(lds + KV0 + (2 + pr) * T, IC<pr>{}, PAR, IC<1>{});
 #endif
-        rescale();
+        rescale(j == 0);
         FA_STAMP(sc_);
         dma_wait();  // K_{j+1}, V_j landed
         FA_STAMP(sd);
@@ -1500,7 +1504,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         mask(S[0][0], S[0][1], mw + r, key0);
         mask(S[0][2], S[0][3], mw + 32 + r, key0);
         sm1_all(IC<0>{});
-        rescale();
+        rescale(j == 0);
         sm2_all(IC<0>{});
         phase2(V, IC<0>{}, IC<0>{}, IC<0>{});
         dma_wait();
