@@ -12,7 +12,11 @@
 // 16x16 row max needs cross-lane steps only on the rare rescale, like the 32x32 one.)
 // Modes: 0 = MFMAs only, 1 = MFMAs + softmax VALU interleaved evenly (one unit per gap group),
 // 2 = as 1 without the exp-argument fma (what folding the scale / max into the MFMA would save),
-// 3 = as 2 without the row-sum add as well.
+// 3 = as 2 without the row-sum add as well; 4 = mode 1's VALU as one block between the MFMA phases.
+// W8 rows: two waves per SIMD (512-thread workgroups), each with HALF the rows (32 queries per
+// wave: 16 + 16 MFMAs and 32 softmax units per tile), waves 4-7 one phase behind waves 0-3: the
+// same work per SIMD as one W4 wave, to see whether two waves interleave the VALU with the MFMAs
+// better than one (a single wave issues a VALU op every 4 cycles at most; the SIMD every 2).
 // Prints TFLOP/s (MFMA FLOPs), cycles per tile and the in-kernel clock, per shape and mode,
 // interleaved repetitions on one device.
 #include <hip/hip_runtime.h>
@@ -65,11 +69,12 @@ struct Sm {
     float sc, msc, l, mx;
 };
 
-template <int SHAPE, int MODE>
-__global__ __launch_bounds__(256, 1) void tile_loop(const int tiles, const uint32_t *seed, float *sink,
-                                                    unsigned long long *clk) {
+template <int SHAPE, int MODE, int WAVES = 4>
+__global__ __launch_bounds__(64 * WAVES, 1) void tile_loop(const int tiles, const uint32_t *seed, float *sink,
+                                                           unsigned long long *clk) {
     const int lane = threadIdx.x & 63;
-    const uint32_t s0 = seed[blockIdx.x * 256 + threadIdx.x];
+    const uint32_t s0 = seed[(blockIdx.x * 512 + threadIdx.x) & 0xffff];
+    constexpr int HALF = WAVES == 8 ? 2 : 1;  // rows per wave: 64 / HALF
     // operand fragments: random fp16 in (-1, 1) (random data: the clock the chip holds depends on the
     // operand values, MI355X_MICROARCH 'DVFS give-back'); S = K.Q^T then has a std of ~2 (D = 128)
     u32x4 kf[4], qf[4], vf[4];
@@ -85,23 +90,24 @@ __global__ __launch_bounds__(256, 1) void tile_loop(const int tiles, const uint3
         qf[i] = (u32x4){rnd(), rnd(), rnd(), rnd()};
         vf[i] = (u32x4){rnd(), rnd(), rnd(), rnd()};
     }
-    constexpr int NS = SHAPE == 32 ? 4 : 16;   // S accumulators per lane (64 floats)
-    constexpr int NO = SHAPE == 32 ? 8 : 32;   // O accumulators per lane (128 floats)
+    constexpr int NS = (SHAPE == 32 ? 4 : 16) / HALF;   // S accumulators per lane (64 floats)
+    constexpr int NO = (SHAPE == 32 ? 8 : 32) / HALF;   // O accumulators per lane (128 floats)
+    constexpr int NU = 32 / HALF;                       // softmax units per phase
     typedef typename std::conditional<SHAPE == 32, f32x16, f32x4>::type acc_t;
     constexpr int AL = SHAPE == 32 ? 16 : 4;
     acc_t S[2][NS], O[NO];
-    uint32_t P[32];
+    uint32_t P[32 / HALF];
 #pragma unroll
     for (int i = 0; i < NS; ++i) { S[0][i] = (acc_t){}; S[1][i] = (acc_t){}; }
 #pragma unroll
     for (int i = 0; i < NO; ++i) O[i] = (acc_t){};
 #pragma unroll
-    for (int i = 0; i < 32; ++i) P[i] = s0 + i;
+    for (int i = 0; i < 32 / HALF; ++i) P[i] = s0 + i;
     Sm st{1.0f, 0.5f, 0.f, -1e30f};  // exp2 arguments ~ N(-0.5, 2): P in a realistic range
-    constexpr int G = SHAPE == 32 ? 32 : 64;   // MFMAs per phase
+    constexpr int G = (SHAPE == 32 ? 32 : 64) / HALF;   // MFMAs per phase
     const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 
-    auto body = [&](auto PAR) {
+    auto ph1 = [&](auto PAR) {
         constexpr int c = decltype(PAR)::value, pc = c ^ 1;
         // phase 1: S[c] = K.Q^T (G MFMAs) || softmax units 0..31 of S[pc]
         static_for<G>([&](auto GG) {
@@ -110,14 +116,14 @@ __global__ __launch_bounds__(256, 1) void tile_loop(const int tiles, const uint3
             if constexpr (SHAPE == 32) mfma32<(g < NS)>(S[c][g % NS], kf[g & 3], qf[(g >> 2) & 3]);
             else mfma16<(g < NS)>(S[c][g % NS], kf[g & 3], qf[(g >> 2) & 3]);
             FENCE();
-            if constexpr (MODE >= 1) {
-                static_for<32>([&](auto UU) {
+            if constexpr (MODE >= 1 && MODE <= 3) {
+                static_for<NU>([&](auto UU) {
                     constexpr int u = decltype(UU)::value;
-                    if constexpr ((u * G) / 32 == g) {
-                        float e = MODE >= 2 ? __builtin_amdgcn_exp2f(S[pc][u / AL][u % AL])
+                    if constexpr ((u * G) / NU == g) {
+                        float e = (MODE >= 2 && MODE <= 3) ? __builtin_amdgcn_exp2f(S[pc][u / AL][u % AL])
                                             : __builtin_amdgcn_exp2f(__builtin_fmaf(S[pc][u / AL][u % AL], st.sc, -st.msc));
                         pin(e);
-                        if constexpr (MODE <= 2) {
+                        if constexpr (MODE <= 2 || MODE == 4) {
                             st.l += e;
                             pin(st.l);
                         }
@@ -125,38 +131,7 @@ __global__ __launch_bounds__(256, 1) void tile_loop(const int tiles, const uint3
                         if constexpr (u & 1) {
                             uint32_t w = pack(S[pc][(u - 1) / AL][(u - 1) % AL], e);
                             pin(w);
-                            P[u >> 1] = w;
-                            st.mx = fmaxf(st.mx, fmaxf(S[c ^ 1][(u - 1) / AL][(u - 1) % AL], e));
-                            pin(st.mx);
-                        }
-                    }
-                });
-            }
-            FENCE();
-        });
-        // phase 2: O += V.P (G MFMAs) || softmax units 32..63 of S[pc]
-        static_for<G>([&](auto GG) {
-            constexpr int g = decltype(GG)::value;
-            u32x4 pb = (u32x4){P[(4 * g) & 31], P[(4 * g + 1) & 31], P[(4 * g + 2) & 31], P[(4 * g + 3) & 31]};
-            if constexpr (SHAPE == 32) mfma32a(O[g % NO], vf[g & 3], pb);
-            else mfma16a(O[g % NO], vf[g & 3], pb);
-            FENCE();
-            if constexpr (MODE >= 1) {
-                static_for<32>([&](auto UU) {
-                    constexpr int u = 32 + decltype(UU)::value;
-                    if constexpr (((u - 32) * G) / 32 == g) {
-                        float e = MODE >= 2 ? __builtin_amdgcn_exp2f(S[pc][u / AL][u % AL])
-                                            : __builtin_amdgcn_exp2f(__builtin_fmaf(S[pc][u / AL][u % AL], st.sc, -st.msc));
-                        pin(e);
-                        if constexpr (MODE <= 2) {
-                            st.l += e;
-                            pin(st.l);
-                        }
-                        S[pc][u / AL][u % AL] = e;
-                        if constexpr (u & 1) {
-                            uint32_t w = pack(S[pc][(u - 1) / AL][(u - 1) % AL], e);
-                            pin(w);
-                            P[(u >> 1) & 31] = w;
+                            P[(u >> 1) % (32 / HALF)] = w;
                             st.mx = fmaxf(st.mx, fmaxf(S[c ^ 1][(u - 1) / AL][(u - 1) % AL], e));
                             pin(st.mx);
                         }
@@ -166,9 +141,69 @@ __global__ __launch_bounds__(256, 1) void tile_loop(const int tiles, const uint3
             FENCE();
         });
     };
+    auto ph2 = [&](auto PAR) {
+        constexpr int c = decltype(PAR)::value, pc = c ^ 1;
+        // phase 2: O += V.P (G MFMAs) || softmax units 32..63 of S[pc]
+        static_for<G>([&](auto GG) {
+            constexpr int g = decltype(GG)::value;
+            constexpr int NP_ = 32 / HALF;
+            u32x4 pb = (u32x4){P[(4 * g) % NP_], P[(4 * g + 1) % NP_], P[(4 * g + 2) % NP_], P[(4 * g + 3) % NP_]};
+            if constexpr (SHAPE == 32) mfma32a(O[g % NO], vf[g & 3], pb);
+            else mfma16a(O[g % NO], vf[g & 3], pb);
+            FENCE();
+            if constexpr (MODE >= 1 && MODE <= 3) {
+                static_for<NU>([&](auto UU) {
+                    constexpr int u = NU + decltype(UU)::value;
+                    if constexpr (((u - NU) * G) / NU == g) {
+                        float e = (MODE >= 2 && MODE <= 3) ? __builtin_amdgcn_exp2f(S[pc][u / AL][u % AL])
+                                            : __builtin_amdgcn_exp2f(__builtin_fmaf(S[pc][u / AL][u % AL], st.sc, -st.msc));
+                        pin(e);
+                        if constexpr (MODE <= 2 || MODE == 4) {
+                            st.l += e;
+                            pin(st.l);
+                        }
+                        S[pc][u / AL][u % AL] = e;
+                        if constexpr (u & 1) {
+                            uint32_t w = pack(S[pc][(u - 1) / AL][(u - 1) % AL], e);
+                            pin(w);
+                            P[(u >> 1) % (32 / HALF)] = w;
+                            st.mx = fmaxf(st.mx, fmaxf(S[c ^ 1][(u - 1) / AL][(u - 1) % AL], e));
+                            pin(st.mx);
+                        }
+                    }
+                });
+            }
+            FENCE();
+        });
+    };
+    // MODE 4: the same units as MODE 1, but as one VALU block between the two MFMA phases (no
+    // interleaving inside a wave: with two waves per SIMD the partner's MFMAs fill the block)
+    auto smblock = [&](auto PAR) {
+        constexpr int c = decltype(PAR)::value, pc = c ^ 1;
+        static_for<2 * NU>([&](auto UU) {
+            constexpr int u = decltype(UU)::value;
+            float e = __builtin_amdgcn_exp2f(__builtin_fmaf(S[pc][u / AL][u % AL], st.sc, -st.msc));
+            pin(e);
+            st.l += e;
+            pin(st.l);
+            S[pc][u / AL][u % AL] = e;
+            if constexpr (u & 1) {
+                uint32_t w = pack(S[pc][(u - 1) / AL][(u - 1) % AL], e);
+                pin(w);
+                P[(u >> 1) % (32 / HALF)] = w;
+                st.mx = fmaxf(st.mx, fmaxf(S[c ^ 1][(u - 1) / AL][(u - 1) % AL], e));
+                pin(st.mx);
+            }
+        });
+    };
+    if (WAVES == 8 && threadIdx.x >= 256) ph2(std::integral_constant<int, 1>{});  // stagger: one phase behind
     for (int t = 0; t < tiles; t += 2) {
-        body(std::integral_constant<int, 0>{});
-        body(std::integral_constant<int, 1>{});
+        ph1(std::integral_constant<int, 0>{});
+        if constexpr (MODE == 4) smblock(std::integral_constant<int, 0>{});
+        ph2(std::integral_constant<int, 0>{});
+        ph1(std::integral_constant<int, 1>{});
+        if constexpr (MODE == 4) smblock(std::integral_constant<int, 1>{});
+        ph2(std::integral_constant<int, 1>{});
     }
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" ::: "memory");
     const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
@@ -181,7 +216,7 @@ __global__ __launch_bounds__(256, 1) void tile_loop(const int tiles, const uint3
     for (int i = 0; i < NS; ++i)
 #pragma unroll
         for (int j = 0; j < AL; ++j) acc += S[0][i][j] + S[1][i][j];
-    sink[blockIdx.x * 256 + threadIdx.x] = acc;
+    sink[blockIdx.x * 512 + threadIdx.x] = acc;
     if (threadIdx.x == 0) {
         clk[2 * blockIdx.x] = t1 - t0;
         clk[2 * blockIdx.x + 1] = r1 - r0;
@@ -199,20 +234,25 @@ int main(int argc, char **argv) {
     uint32_t *seed;
     float *sink;
     unsigned long long *clk;
-    CK(hipMalloc(&seed, nwg * 256 * 4));
-    CK(hipMalloc(&sink, nwg * 256 * 4));
+    CK(hipMalloc(&seed, 65536 * 4));
+    CK(hipMalloc(&sink, nwg * 512 * 4));
     CK(hipMalloc(&clk, nwg * 16));
-    std::vector<uint32_t> h(nwg * 256);
+    std::vector<uint32_t> h(65536);
     uint32_t x = 12345;
     for (auto &v : h) { x = x * 1664525u + 1013904223u; v = x; }
     CK(hipMemcpy(seed, h.data(), h.size() * 4, hipMemcpyHostToDevice));
     typedef void (*K)(int, const uint32_t *, float *, unsigned long long *);
-    constexpr int NK = 8;
+    constexpr int NK = 14;
     const K ks[NK] = {tile_loop<32, 0>, tile_loop<32, 1>, tile_loop<32, 2>, tile_loop<32, 3>,
-                      tile_loop<16, 0>, tile_loop<16, 1>, tile_loop<16, 2>, tile_loop<16, 3>};
+                      tile_loop<16, 0>, tile_loop<16, 1>, tile_loop<16, 2>, tile_loop<16, 3>,
+                      tile_loop<32, 0, 8>, tile_loop<32, 1, 8>, tile_loop<16, 0, 8>, tile_loop<16, 1, 8>,
+                      tile_loop<32, 4, 4>, tile_loop<32, 4, 8>};
+    const int waves[NK] = {4, 4, 4, 4, 4, 4, 4, 4, 8, 8, 8, 8, 4, 8};
     const char *names[NK] = {"32x32x16 MFMA only", "32x32x16 + softmax VALU", "32x32x16 softmax -fma",
                              "32x32x16 softmax -fma -add", "16x16x32 MFMA only", "16x16x32 + softmax VALU",
-                             "16x16x32 softmax -fma", "16x16x32 softmax -fma -add"};
+                             "16x16x32 softmax -fma", "16x16x32 softmax -fma -add", "W8 32x32x16 MFMA only",
+                             "W8 32x32x16 + softmax", "W8 16x16x32 MFMA only", "W8 16x16x32 + softmax",
+                             "32x32x16 softmax block", "W8 32x32x16 softmax block"};
     const double flop_per_tile = 2.0 * 2 * 64 * 64 * 128;  // S and P.V per wave
     std::vector<std::vector<double>> tf(NK), cyc(NK), ghz(NK);
     hipEvent_t a, b;
@@ -220,13 +260,13 @@ int main(int argc, char **argv) {
     CK(hipEventCreate(&b));
     // warm-up: ~2 s of launches (the clock settles, MI355X_MICROARCH 'DVFS give-back')
     for (int w = 0; w < 8; ++w)
-        for (int k = 0; k < NK; ++k) hipLaunchKernelGGL(ks[k], dim3(nwg), dim3(256), 0, 0, tiles, seed, sink, clk);
+        for (int k = 0; k < NK; ++k) hipLaunchKernelGGL(ks[k], dim3(nwg), dim3(64 * waves[k]), 0, 0, tiles, seed, sink, clk);
     CK(hipDeviceSynchronize());
     std::vector<unsigned long long> hc(nwg * 2);
     for (int r = 0; r < reps; ++r)
         for (int k = 0; k < NK; ++k) {
             CK(hipEventRecord(a));
-            hipLaunchKernelGGL(ks[k], dim3(nwg), dim3(256), 0, 0, tiles, seed, sink, clk);
+            hipLaunchKernelGGL(ks[k], dim3(nwg), dim3(64 * waves[k]), 0, 0, tiles, seed, sink, clk);
             CK(hipEventRecord(b));
             CK(hipEventSynchronize(b));
             float ms;
@@ -239,6 +279,7 @@ int main(int argc, char **argv) {
             }
             std::sort(cy.begin(), cy.end());
             std::sort(gh.begin(), gh.end());
+            // per SIMD and tile: 64 query rows either way (W8: two waves of 32 rows)
             tf[k].push_back(flop_per_tile * tiles * 4.0 * nwg / (ms * 1e-3) / 1e12);
             cyc[k].push_back(cy[nwg / 2]);
             ghz[k].push_back(gh[nwg / 2]);
