@@ -1,7 +1,8 @@
 """Build gate on the device assembly of every kernel instantiation (called by ``_build.build_abi``).
 
 ``fa_fwd_w4`` keeps O (a0..a127) and the Q fragments (a128..a191) in literal AGPRs that only its
-inline asm reads and writes (csrc/fa_agpr_asm.inc). The compiler does not know these registers are
+inline asm reads and writes (csrc/fa_agpr_asm.inc); ``fa_fwd_p8`` likewise O (a0..a63) and Q
+(a64..a95). The compiler does not know these registers are
 live across the separate asm statements, so a compiler-generated AGPR use in that range (for example
 a VGPR spill to an AGPR after a toolchain or code change) would silently corrupt the output. This
 module scans the ``-save-temps`` assembly: any use of those AGPRs (a0..a63 at D = 64) outside ``;;#ASMSTART``/``;;#ASMEND``
@@ -19,6 +20,14 @@ _REG = re.compile(r"\ba\[(\d+)(?::\d+)?\]|\ba(\d+)\b")
 _TILE = re.compile(r"ELi(64|128)ELb")  # the head-dim tile template argument of the mangled name
 
 
+def pinned_p8(fn: str, reg: int) -> bool:
+    """fa_fwd_p8 (256 registers per wave): O^T of its one 32-row block in a0..a(D/2 - 1), the Q
+    fragments in a64..a95 (a64..a79 at D = 64)."""
+    m = _TILE.search(fn)
+    d = int(m.group(1)) if m else 128
+    return reg < d // 2 or 64 <= reg < 64 + d // 4
+
+
 def pinned(fn: str, reg: int) -> bool:
     """a0..a(head-dim tile - 1) hold O^T of both 32-row blocks (D/32 d-tiles x 16 each x 2 blocks),
     a128..a191 the Q fragments; at D = 64 the compiler may use a64..a127."""
@@ -33,7 +42,7 @@ def agpr_violations(text: str) -> list[str]:
     for ln in text.splitlines():
         m = re.match(r"^(_Z\S*):", ln)
         if m:
-            fn = m.group(1) if m.group(1).startswith("_ZN2fa9fa_fwd_w4") else None
+            fn = m.group(1) if m.group(1).startswith(("_ZN2fa9fa_fwd_w4", "_ZN2fa9fa_fwd_p8")) else None
             continue
         if ";;#ASMSTART" in ln:
             in_asm = True
@@ -41,7 +50,8 @@ def agpr_violations(text: str) -> list[str]:
             in_asm = False
         elif fn and not in_asm and not ln.lstrip().startswith(";"):
             for r in _REG.finditer(ln.split(";")[0]):
-                if pinned(fn, int(r.group(1) or r.group(2))):
+                rule = pinned_p8 if fn.startswith("_ZN2fa9fa_fwd_p8") else pinned
+                if rule(fn, int(r.group(1) or r.group(2))):
                     bad.append(f"{fn}: {ln.strip()}")
                     break
     return bad

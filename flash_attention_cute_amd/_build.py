@@ -122,6 +122,10 @@ def build_abi(force: bool = False, verbose: bool = False, stamps: bool = False, 
     from ._asm_check import check_file
 
     problems = [p for a in asm_files for p in check_file(a)]
+    if diag:  # stamp / experiment builds: spills are reported, not fatal (the AGPR rule stays)
+        for q in [q for q in problems if "vgpr_spill_count" in q]:
+            print(f"warning ({sdir}): {q}", flush=True)
+        problems = [q for q in problems if "vgpr_spill_count" not in q]
     for a in asm_files:  # keep the .s for inspection, drop the large intermediates
         for junk in a.parent.glob("fa_inst*"):
             if junk.suffix in (".bc", ".hipi", ".out", ".txt", ".hipfb") or junk.name.endswith("resolution.txt"):

@@ -36,7 +36,8 @@ thread_local int g_last_path = fa::kPathNone;
 
 fa::Knobs knobs_from_env() {
     fa::Knobs k{0, 0, 1, fa::kDecTargetWgs, fa::kDecNt};
-    if (const char *v = getenv("FA_GFX950_VARIANT")) k.variant = !strcmp(v, "w8") ? 1 : !strcmp(v, "w4slow") ? 2 : 0;
+    if (const char *v = getenv("FA_GFX950_VARIANT"))
+        k.variant = !strcmp(v, "w8") ? 1 : !strcmp(v, "w4slow") ? 2 : !strcmp(v, "p8") ? 3 : 0;
     if (const char *e = getenv("FA_W4_GRID")) k.w4_grid = atoll(e) > 0 ? atoll(e) : 0;
     if (const char *e = getenv("FA_GFX950_DECODE")) k.decode = strcmp(e, "0") != 0;
     if (const char *e = getenv("FA_DEC_TARGET_WGS")) k.dec_target = atoll(e) > 0 ? atoll(e) : fa::kDecTargetWgs;
@@ -291,7 +292,7 @@ extern "C" int fa_fwd_gfx950_geometry(const fa_fwd_params *params, int causal, i
     const int64_t n_qtiles = (params->seqlen_q + fa::kBlockM - 1) / fa::kBlockM;
     if (block_m) *block_m = fa::kBlockM;
     if (block_n) *block_n = fa::kBlockN;
-    if (threads) *threads = (fa::variant_from_env() == 1 ? fa::kThreads : 256);
+    if (threads) *threads = (fa::variant_from_env() == 1 || fa::variant_from_env() == 3 ? fa::kThreads : 256);
     if (workgroups) *workgroups = n_qtiles * params->num_heads_q * params->batch_size;
     return FA_OK;
 }

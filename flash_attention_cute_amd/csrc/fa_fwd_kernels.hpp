@@ -1609,14 +1609,19 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 }
 #undef FA_STAMP
 
+// the paired 8-wave kernel (fa_fwd_p8.hpp)
+template <class DT, bool C, int kD, bool kExact>
+int launch_p8(const fa_fwd_params &p, hipStream_t stream);
+
 // ---- host launch of one instantiation -------------------------------------------------
 template <class DT, bool C, int kD, bool kExact>
 int launch_one(const fa_fwd_params &p, const int *cu_q, const int *cu_k, const RopeArgs &rope, hipStream_t stream) {
     if (rope.cos && !kExact) return set_err(FA_ERR_UNSUPPORTED, "fused RoPE needs head dim 64 or 128");
     const int64_t n_qtiles = (p.seqlen_q + kBlockM - 1) / kBlockM;
     const int64_t nwg = n_qtiles * p.num_heads_q * p.batch_size;
-    // varlen and fused RoPE always run fa_fwd_w4 (w4slow under the debug variant); w8 has neither
-    const int variant = (cu_q || rope.cos) && variant_from_env() == 1 ? 0 : variant_from_env();
+    // varlen and fused RoPE run fa_fwd_w4 (w4slow under the debug variant); w8 / p8 have neither
+    const int variant = (cu_q || rope.cos) && (variant_from_env() == 1 || variant_from_env() == 3) ? 0 : variant_from_env();
+    if (variant == 3) return launch_p8<DT, C, kD, kExact>(p, stream);
     if (variant == 1)
         hipLaunchKernelGGL((fa_fwd_w8<DT, C, kD, kExact>), dim3((uint32_t)nwg), dim3(kThreads), 0, stream, p,
                            (int)n_qtiles);

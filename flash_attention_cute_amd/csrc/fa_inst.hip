@@ -3,6 +3,7 @@
 // FA_INST_EXACT (0 | 1), in parallel, and links the objects with fa_fwd_gfx950.hip.
 #ifndef FA_INST_STUB
 #include "fa_fwd_kernels.hpp"
+#include "fa_fwd_p8.hpp"
 #include "fa_decode.hpp"
 #else
 // diagnostic builds that only need some instantiations (_build.build_abi(only=...)): the others

@@ -28,7 +28,8 @@ int set_err(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3))
 // the command line), and can be changed afterwards only through fa_debug_set_knobs (tests).
 //   variant    0 = fa_fwd_w4 (default); 1 = fa_fwd_w8 (FA_GFX950_VARIANT=w8: the 8-wave
 //              register-staged kernel, A/B and cross-check); 2 = w4 without its pipelined body
-//              (FA_GFX950_VARIANT=w4slow, debug)
+//              (FA_GFX950_VARIANT=w4slow, debug); 3 = fa_fwd_p8 (FA_GFX950_VARIANT=p8: two waves per
+//              SIMD, dense prefill; varlen / RoPE stay on fa_fwd_w4)
 //   w4_grid    cap of the persistent fa_fwd_w4 grid (FA_W4_GRID; 0 = the CU count)
 //   decode     split-KV decode kernel for few rows per kv-head (FA_GFX950_DECODE=0 turns it off)
 //   dec_target workgroups the decode split plan aims at (FA_DEC_TARGET_WGS)
@@ -44,7 +45,7 @@ const Knobs &knobs();
 inline int variant_from_env() { return knobs().variant; }
 
 // Which kernel the last fa_fwd_gfx950* call on this thread launched (fa_debug_last_path)
-enum Path { kPathNone = 0, kPathW4 = 1, kPathW8 = 2, kPathW4Slow = 3, kPathDecode = 4, kPathDecodeSplit = 5 };
+enum Path { kPathNone = 0, kPathW4 = 1, kPathW8 = 2, kPathW4Slow = 3, kPathDecode = 4, kPathDecodeSplit = 5, kPathP8 = 6 };
 void set_last_path(int path);
 
 // diagnostic per-wave phase stamps of fa_fwd_w4 (only a -DFA_STAMPS=1 build writes them; see

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Interleaved A/B timing of several builds of the C-ABI library on one bench config (same process,
 same device, same inputs), so device-to-device clock differences cancel out.
-usage: python scripts/ab_libs.py <cfg> <lib.so> [<lib.so> ...]   (env AB_REPS, AB_ITERS)
+usage: python scripts/ab_libs.py <cfg> <lib.so>[@variant] [...]   (env AB_REPS, AB_ITERS)
+       variant: w4 | w8 | w4slow | p8, set through the library's fa_debug_set_knobs before its runs
 """
 import ctypes
 import os
@@ -15,7 +16,10 @@ sys.path.insert(0, str(ROOT))
 import bench  # noqa: E402
 
 cfg = bench.CONFIGS[sys.argv[1]]
-libs = [ctypes.CDLL(os.path.abspath(p)) for p in sys.argv[2:]]
+VARIANTS = {"w4": 0, "w8": 1, "w4slow": 2, "p8": 3}
+specs = [a.split("@") for a in sys.argv[2:]]
+libs = [ctypes.CDLL(os.path.abspath(sp[0])) for sp in specs]
+variants = [VARIANTS[sp[1]] if len(sp) > 1 else -1 for sp in specs]
 
 
 class P(ctypes.Structure):
@@ -46,6 +50,7 @@ dcode = 0 if dt == torch.float16 else 1
 
 
 def run(i, n):
+    libs[i].fa_debug_set_knobs(variants[i], -1, -1, -1, -1)
     for _ in range(n):
         assert libs[i].fa_fwd_gfx950(ctypes.byref(ps[i]), dcode, int(cfg["causal"]), ctypes.c_void_p(stream)) == 0
 

@@ -6,7 +6,7 @@ Loads build/stamps/libfa_gfx950.so through its C-ABI, runs ~2 s of back-to-back 
 bench config (DVFS settles), then one stamped launch, and prints per-wave medians of the cycle
 split: phase 1 (S = K.Q^T || softmax 2 || DMA), phase 2 (O += P.V || softmax 1) + rescale, the
 DMA wait, the barrier; plus the in-kernel clock (s_memtime / s_memrealtime x 100 MHz).
-usage: python scripts/stamps.py [c2|c3|c4|c5]
+usage: python scripts/stamps.py [c2|c3|c4|c5] [w4|p8]   (p8: 8 waves per Q block; p1 = phase A, p2 = B)
 """
 import ctypes
 import sys
@@ -19,6 +19,8 @@ sys.path.insert(0, str(ROOT))
 import bench  # noqa: E402
 
 cfg = bench.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "c2"]
+variant = sys.argv[2] if len(sys.argv) > 2 else "w4"
+WAVES = 8 if variant == "p8" else 4
 import os  # noqa: E402
 
 lib = ctypes.CDLL(os.environ.get("FA_STAMPS_LIB", str(ROOT / "build" / "stamps" / "libfa_gfx950.so")))
@@ -45,9 +47,10 @@ p = P(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), cfg["B"], cfg["Hq"
       *[t.stride(0) for t in st], *[t.stride(1) for t in st], *[t.stride(2) for t in st],
       cfg["D"] ** -0.5 * 1.4426950408889634)
 nwg = cfg["B"] * cfg["Hq"] * ((cfg["Sq"] + 255) // 256)
-buf = torch.zeros(nwg * 4 * 12, dtype=torch.int64, device=dev)
+buf = torch.zeros(nwg * WAVES * 12, dtype=torch.int64, device=dev)
 stream = torch.cuda.current_stream().cuda_stream
 lib.fa_debug_set_stamps(ctypes.c_void_p(0))
+lib.fa_debug_set_knobs({"w4": 0, "p8": 3}[variant], -1, -1, -1, -1)
 import time  # noqa: E402
 
 t0 = time.time()
@@ -66,7 +69,7 @@ lib.fa_debug_set_stamps(ctypes.c_void_p(0))
 s = buf.view(-1, 12).cpu().double()
 names = ["total", "p1", "p2+resc", "dma_wait", "barrier", "tiles", "drain", "prologue", "epilogue", "realtime"]
 med = s.median(dim=0).values
-print(f"{cfg['workload']}: {n} warm launches, {s.shape[0]} waves")
+print(f"{cfg['workload']} [{variant}]: {n} warm launches, {s.shape[0]} waves")
 for i, nm in enumerate(names):
     print(f"  {nm:10s} median {med[i]:12.0f}  mean {s[:, i].mean():12.0f}")
 tiles = s[:, 5].clamp(min=1)
@@ -80,3 +83,12 @@ print(f"  launch span {float((s[:, 10] + s[:, 0]).max() - s[:, 10].min()):.0f} c
 for i, nm in [(6, "drain"), (7, "prologue"), (8, "epilogue")]:
     qs = torch.quantile(s[:, i], torch.tensor([0.1, 0.5, 0.9, 0.99], dtype=torch.float64))
     print(f"  {nm:10s} p10 {qs[0]:8.0f}  p50 {qs[1]:8.0f}  p90 {qs[2]:8.0f}  p99 {qs[3]:8.0f}")
+if WAVES == 8:  # leaders (waves 0-3) and followers (4-7) of every block
+    w = torch.arange(s.shape[0]) % 8
+    for nm, sel in (("leaders", w < 4), ("followers", w >= 4)):
+        ss = s[sel]
+        t = ss[:, 5].clamp(min=1)
+        print(f"  {nm}: per tile A {float((ss[:, 1] / t).median()):.0f}  B {float((ss[:, 2] / t).median()):.0f}"
+              f"  wait {float((ss[:, 3] / t).median()):.0f}  barrier {float((ss[:, 4] / t).median()):.0f}"
+              f"  drain {float(ss[:, 6].median()):.0f}  prologue {float(ss[:, 7].median()):.0f}"
+              f"  epilogue {float(ss[:, 8].median()):.0f}")

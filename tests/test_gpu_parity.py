@@ -29,11 +29,12 @@ pytestmark = pytest.mark.gpu
 TOL = {torch.float16: (2e-3, 2e-3, 1e-4), torch.bfloat16: (1.6e-2, 1.6e-2, 1e-3)}
 
 
-@pytest.fixture(params=["w4", "w8", "w4slow"])
+@pytest.fixture(params=["w4", "w8", "w4slow", "p8"])
 def fa(device, request):
     """The public op with one kernel variant selected (the product default w4, the 8-wave cross-check
-    w8, the non-pipelined debug body w4slow) through the debug knob hook. Function-scoped: the knobs
-    are restored to their defaults after every test, so no later test inherits a variant."""
+    w8, the non-pipelined debug body w4slow, the paired 8-wave p8) through the debug knob hook.
+    Function-scoped: the knobs are restored to their defaults after every test, so no later test
+    inherits a variant."""
     import flash_attention_cute_amd as m
     from flash_attention_cute_amd import _debug
     from flash_attention_cute_amd import flash_attention as fam

@@ -6,7 +6,7 @@ launches of the same inputs. DESIGN.md section 5 records one discarded experimen
 524k differed; this sweep checks ~0.8M rows of the kept kernel (fa_fwd_w4, persistent, several Q
 blocks per workgroup through a capped grid so every block switch -- Q staged by LDS-DMA, the
 first-tile rescale -- runs many times) and requires every row within the parity tolerance and two
-launches bit-identical.
+launches bit-identical. The same sweep runs the paired 8-wave variant fa_fwd_p8.
 """
 from __future__ import annotations
 
@@ -20,14 +20,17 @@ pytestmark = pytest.mark.gpu
 SEEDS = range(12)
 
 
-@pytest.fixture
-def op(device):
+@pytest.fixture(params=["w4", "p8"])
+def op(device, request):
     from flash_attention_cute_amd import _debug
     from flash_attention_cute_amd import flash_attention as fam
     from flash_attention_cute_amd import flash_attn_func
 
     assert fam.flash_attention_cuda is not None, f"gfx950 extension failed to load: {fam._load_error!r}"
-    _debug.set_knobs(w4_grid=16)  # 16 workgroups: each walks 4 Q blocks (3 block switches)
+    # 16 workgroups: each walks 4 Q blocks (3 block switches); the product kernel and the paired
+    # 8-wave variant
+    _debug.set_knobs(variant=request.param, w4_grid=16)
+    flash_attn_func.variant = request.param
     try:
         yield flash_attn_func
     finally:
@@ -45,6 +48,6 @@ def test_seed_sweep_every_row(op, device, dtype, causal):
         out = op(qd, kd, vd, causal=causal)
         again = op(qd, kd, vd, causal=causal)
         torch.cuda.synchronize()
-        assert _debug.last_path() == "w4"
+        assert _debug.last_path() == op.variant
         assert torch.equal(out, again), f"seed {seed}: two launches differ"
         check(out, q, k, v, 128 ** -0.5, causal, dtype)
