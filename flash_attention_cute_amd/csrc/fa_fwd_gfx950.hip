@@ -145,12 +145,12 @@ int check_params(const fa_fwd_params *p, int dtype, int causal) {
 // runs every D <= 128 on its 128 kernel, csrc/kernel_dispatcher.h:45-52)
 template <class DT, bool C>
 int launch(const fa_fwd_params &p, hipStream_t stream, const int *cu_q = nullptr, const int *cu_k = nullptr,
-           const fa::RopeArgs &rope = fa::RopeArgs{nullptr, nullptr, 0, 0}) {
+           const fa::PathArgs &xa = fa::PathArgs{nullptr, nullptr, 0, 0, -1}) {
     if (p.headdim <= 64)
-        return p.headdim == 64 ? launch_one<DT, C, 64, true>(p, cu_q, cu_k, rope, stream)
-                               : launch_one<DT, C, 64, false>(p, cu_q, cu_k, rope, stream);
-    return p.headdim == 128 ? launch_one<DT, C, 128, true>(p, cu_q, cu_k, rope, stream)
-                            : launch_one<DT, C, 128, false>(p, cu_q, cu_k, rope, stream);
+        return p.headdim == 64 ? launch_one<DT, C, 64, true>(p, cu_q, cu_k, xa, stream)
+                               : launch_one<DT, C, 64, false>(p, cu_q, cu_k, xa, stream);
+    return p.headdim == 128 ? launch_one<DT, C, 128, true>(p, cu_q, cu_k, xa, stream)
+                            : launch_one<DT, C, 128, false>(p, cu_q, cu_k, xa, stream);
 }
 template <class DT, bool C>
 int launch_dec(const fa_fwd_params &p, const fa::DecArgs &a, void *ws, hipStream_t stream) {
@@ -228,7 +228,7 @@ int dispatch_rope(const fa_rope_fwd_params *r, int dtype, int causal, void *stre
         return set_err(FA_ERR_INVALID_ARGUMENT, "RoPE tables must be 16-byte aligned with strides multiple of 8");
     if (r->rope_seqlen_stride < 0 || r->rope_seqlen_stride * 2 * 64 + 256 > 0x7fffffffLL)
         return set_err(FA_ERR_UNSUPPORTED, "RoPE seqlen stride too large for 32-bit tile offsets");
-    const fa::RopeArgs ra{r->rope_cos, r->rope_sin, r->rope_batch_stride, r->rope_seqlen_stride};
+    const fa::PathArgs ra{r->rope_cos, r->rope_sin, r->rope_batch_stride, r->rope_seqlen_stride, -1};
     hipStream_t s = (hipStream_t)stream;
     if (dtype == FA_DTYPE_F16)
         return causal ? launch<fa::F16, true>(r->base, s, nullptr, nullptr, ra)
@@ -237,7 +237,36 @@ int dispatch_rope(const fa_rope_fwd_params *r, int dtype, int causal, void *stre
                   : launch<fa::BF16, false>(r->base, s, nullptr, nullptr, ra);
 }
 
+// Local (sliding) window: keys below the first row's window are cut off the problem (views of k /
+// v, so the kernel never fetches them); if the window then cuts nothing more, the plain path runs
+// (including the split-KV decode kernel), else fa_fwd_w4 with the window mask.
+int dispatch_window(const fa_fwd_params *params, int dtype, int causal, int64_t window_left, void *stream) {
+    g_last_path = fa::kPathNone;
+    const int rc = check_params(params, dtype, causal);
+    if (rc != FA_OK) return rc;
+    if (window_left < 0) return dispatch(params, dtype, causal, nullptr, 0, stream);
+    fa_fwd_params p = *params;
+    int64_t cut = p.seqlen_kv - p.seqlen_q - window_left;
+    if (cut > 0) {
+        p.k_ptr = (const char *)p.k_ptr + 2 * cut * p.k_seqlen_stride;
+        p.v_ptr = (const char *)p.v_ptr + 2 * cut * p.v_seqlen_stride;
+        p.seqlen_kv -= cut;
+    }
+    // the last query row's window starts at key Sk' - 1 - window_left: at or before 0, nothing is cut
+    if (p.seqlen_kv - 1 <= window_left) return dispatch(&p, dtype, causal, nullptr, 0, stream);
+    const fa::PathArgs xa{nullptr, nullptr, 0, 0, (int)window_left};
+    hipStream_t s = (hipStream_t)stream;
+    if (dtype == FA_DTYPE_F16)
+        return causal ? launch<fa::F16, true>(p, s, nullptr, nullptr, xa) : launch<fa::F16, false>(p, s, nullptr, nullptr, xa);
+    return causal ? launch<fa::BF16, true>(p, s, nullptr, nullptr, xa) : launch<fa::BF16, false>(p, s, nullptr, nullptr, xa);
+}
+
 }  // namespace
+
+extern "C" int fa_fwd_gfx950_window(const fa_fwd_params *params, int dtype, int causal, int64_t window_left,
+                                    void *stream) {
+    return dispatch_window(params, dtype, causal, window_left, stream);
+}
 
 extern "C" int fa_fwd_gfx950_rope(const fa_rope_fwd_params *params, int dtype, int causal, void *stream) {
     return dispatch_rope(params, dtype, causal, stream);

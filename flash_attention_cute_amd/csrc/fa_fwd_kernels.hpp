@@ -756,7 +756,7 @@ constexpr int vmcnt_enc(int n) { return (n & 15) | (((n >> 4) & 3) << 14) | 0x70
 template <class DT, bool kCausal, int kD, bool kExactD>
 __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const int n_qtiles, const int dbg,
                                                     unsigned long long *stamps, const int *cu_q, const int *cu_k,
-                                                    const RopeArgs rope) {
+                                                    const PathArgs xa) {
     // Diagnostic build only (-DFA_STAMPS=1, scripts/stamps.py): per-wave s_memtime phase totals.
 #ifdef FA_STAMPS
     unsigned long long st_t0 = __builtin_amdgcn_s_memtime(), st_rt0 = __builtin_amdgcn_s_memrealtime();
@@ -843,9 +843,13 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 
     // per-block geometry (set_block)
     const char *qb, *kb, *vb;
-    const char *cosb = nullptr, *sinb = nullptr;  // RoPE tables of this block's sequence (rope.cos)
+    const char *cosb = nullptr, *sinb = nullptr;  // RoPE tables of this block's sequence (xa.cos)
     char *ob;
     int m0, mw, n_end, n_pipe;
+    // local window (xa.window_left >= 0): tiles [j_lo, n_end) hold the block's visible keys, and
+    // tiles below j_um have a score left of some row's window (masked like the diagonal)
+    const int wl = xa.window_left;
+    int j_lo = 0, j_um = 0;
     auto set_block = [&](const Work wk) {
         const int hq = wk.hq, b = wk.b;
         const int hkv = hq / (int)p.head_q_per_group;
@@ -862,10 +866,10 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             krow0 = (int64_t)k0 * p.k_seqlen_stride;
             vrow0 = (int64_t)k0 * p.v_seqlen_stride;
         }
-        if (kExactD && rope.cos) {  // (the host only passes RoPE tables to exact-D instantiations)
-            const int64_t crow0 = cu_q ? (int64_t)cu_q[b] * rope.seq_stride : (int64_t)b * rope.batch_stride;
-            cosb = (const char *)rope.cos + 2 * crow0;
-            sinb = (const char *)rope.sin + 2 * crow0;
+        if (kExactD && xa.cos) {  // (the host only passes RoPE tables to exact-D instantiations)
+            const int64_t crow0 = cu_q ? (int64_t)cu_q[b] * xa.seq_stride : (int64_t)b * xa.batch_stride;
+            cosb = (const char *)xa.cos + 2 * crow0;
+            sinb = (const char *)xa.sin + 2 * crow0;
         }
         qb = (const char *)p.q_ptr + 2 * (qrow0 + (int64_t)hq * p.q_head_stride);
         kb = (const char *)p.k_ptr + 2 * (krow0 + (int64_t)hkv * p.k_head_stride);
@@ -888,6 +892,13 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             n_pipe = min(n_pipe, x <= 0 ? 0 : x / kBlockN);
         }
         n_pipe = min(n_pipe, n_end);
+        j_lo = j_um = 0;
+        if (wl >= 0) {
+            const int lo0 = m0 + diag - wl;                         // the first row's first key
+            const int lo1 = min(m0 + kBlockM, Sq) - 1 + diag - wl;  // the last row's
+            j_lo = min(max(lo0, 0) / kBlockN, n_end);
+            j_um = min((max(lo1, 0) + kBlockN - 1) / kBlockN, n_end);
+        }
     };
     set_block(decode_work<kCausal>(nwg, xcd + 8 * kblk, n_qtiles, (int)p.num_heads_q));
 
@@ -916,13 +927,13 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             });
         }
     };
-    // RoPE fused into the Q load (rope.cos != nullptr, exact D): Q, cos and sin of the wave's 64 rows
+    // RoPE fused into the Q load (xa.cos != nullptr, exact D): Q, cos and sin of the wave's 64 rows
     // into VGPRs, rotate-half in fp32, rounded once to T, then into the Q AGPRs. The rotation partner
     // of chunk 2ks+h is chunk 2(ks +- KS/2)+h -- the same lane. Issued in the block prologue (not
     // under the previous block's drain, whose S / P registers are live) and waited for there.
-    const bool rope_q = kExactD && rope.cos != nullptr;
+    const bool rope_q = kExactD && xa.cos != nullptr;
     auto load_q_rope = [&]() __attribute__((always_inline)) {
-        const int qs = (int)p.q_seqlen_stride, cs = (int)rope.seq_stride;
+        const int qs = (int)p.q_seqlen_stride, cs = (int)xa.seq_stride;
         const int rows = min(Sq - mw, 64);
         const rsrc_t qr = make_rsrc(qb + 2 * (int64_t)mw * qs, slab_bytes(rows, qs, D));
         const rsrc_t cr = make_rsrc(cosb + 2 * (int64_t)mw * cs, slab_bytes(rows, cs, D));
@@ -1009,15 +1020,16 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         kvo[n] = (kExactD || kch * 8 < D) ? row * ks_ * 2 + 16 * kch : 0x7ffffff0;
         vvo[n] = (kExactD || vch * 8 < D) ? row * vs_ * 2 + 16 * vch : 0x7ffffff0;
     }
-    auto stage_k = [&](const int j) {
+    // tile j into ring slot `slot` (the block's tiles alternate slots from j_lo on)
+    auto stage_k = [&](const int j, const int slot) {
         const int key0 = j * kBlockN;
         const rsrc_t kr = make_rsrc(kb + 2 * (int64_t)key0 * ks_, slab_bytes(min(Sk - key0, kBlockN), ks_, D));
-        dma_pieces<NP>(kr, lds_u32(lds + KV0 + (j & 1) * T) + wave * NP * 1024, kvo);
+        dma_pieces<NP>(kr, lds_u32(lds + KV0 + slot * T) + wave * NP * 1024, kvo);
     };
-    auto stage_v = [&](const int j) {
+    auto stage_v = [&](const int j, const int slot) {
         const int key0 = j * kBlockN;
         const rsrc_t vr = make_rsrc(vb + 2 * (int64_t)key0 * vs_, slab_bytes(min(Sk - key0, kBlockN), vs_, D));
-        dma_pieces<NP>(vr, lds_u32(lds + KV0 + (2 + (j & 1)) * T) + wave * NP * 1024, vvo);
+        dma_pieces<NP>(vr, lds_u32(lds + KV0 + (2 + slot) * T) + wave * NP * 1024, vvo);
     };
 
     // ---- per-lane LDS read addresses -----------------------------------------------------
@@ -1371,7 +1383,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         return rows >= kBlockN ? full : slab_bytes(rows, stride, D);
     };
 
-    stage_k(0);  // the first block's K_0 (its Q is in flight above)
+    stage_k(j_lo, 0);  // the first block's first K tile (its Q is in flight above)
     for (;;) {
     // ---- block prologue: Q and K_0 of this block are in flight ------------------------------
 #ifdef FA_STAMPS
@@ -1380,8 +1392,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #pragma unroll
     for (int i = 0; i < 8; ++i) st_acc[i] = 0;
 #endif
-    kp = kb + step_k;
-    vp = vb;
+    kp = kb + (j_lo + 1) * step_k;
+    vp = vb + j_lo * step_v;
     if (rope_q) load_q_rope();
 #pragma unroll
     for (int X = 0; X < 2; ++X) {
@@ -1418,11 +1430,21 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // causal diagonal / Sk tail: scores of keys past a row's last visible key -> kNeg
     auto mask = [&](f32x16 &s0, f32x16 &s1, const int row, const int key0) __attribute__((always_inline)) {
         const int lim = kCausal ? min(Sk - 1, row + diag) : Sk - 1;
+        if (wl < 0) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int kk = key0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-            if (kk > lim) s0[i] = kNeg;
-            if (kk + 32 > lim) s1[i] = kNeg;
+            for (int i = 0; i < 16; ++i) {
+                const int kk = key0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                if (kk > lim) s0[i] = kNeg;
+                if (kk + 32 > lim) s1[i] = kNeg;
+            }
+        } else {  // and keys left of the row's window
+            const int lo = row + diag - wl;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int kk = key0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                if (kk > lim || kk < lo) s0[i] = kNeg;
+                if (kk + 32 > lim || kk + 32 < lo) s1[i] = kNeg;
+            }
         }
     };
     auto iter = [&](const int j, auto PAR, auto MASKED) __attribute__((always_inline)) {
@@ -1452,7 +1474,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #else
         phase2(lds + KV0 + (2 + pr) * T, IC<pr>{}, PAR, IC<1>{});
 #endif
-        rescale(j == 0);
+        rescale(j == j_lo);
         FA_STAMP(sc_);
         dma_wait();  // K_{j+1}, V_j landed
         FA_STAMP(sd);
@@ -1469,15 +1491,27 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // every tile runs pipelined: first the tiles without a masked score, then (a second loop, so
     // the hot loop carries no mask branch) the diagonal / tail tiles with a mask step between the
     // phases. The debug variant (dbg & 1) runs all tiles through the plain body below instead.
-    const int n_loop = (dbg & 1) ? 0 : n_end;
+    // Tile j runs with parity (j - j_lo) & 1 (ring slots and S / P registers). A local window adds
+    // a leading run of masked tiles [j_lo, j_um), rounded up to an even count so the unmasked loop
+    // starts on parity 0.
+    const int n_loop = (dbg & 1) ? j_lo : n_end;
     const int n_unm = min(n_pipe, n_loop);
-    for (int j = 0; j < n_unm; j += 2) {
-        iter(j, IC<0>{}, IC<0>{});
-        if (j + 1 < n_unm) iter(j + 1, IC<1>{}, IC<0>{});
+    int j = j_lo;  // the next tile
+    if (j_um > j_lo) {
+        const int e = min(j_um + ((j_um - j_lo) & 1), n_loop);
+        for (int t = j; t < e; t += 2) {
+            iter(t, IC<0>{}, IC<1>{});
+            if (t + 1 < e) iter(t + 1, IC<1>{}, IC<1>{});
+        }
+        j = max(j, e);
+    }
+    for (int t = j; t < n_unm; t += 2) {
+        iter(t, IC<0>{}, IC<0>{});
+        if (t + 1 < n_unm) iter(t + 1, IC<1>{}, IC<0>{});
     }
     {
-        int j = n_unm;
-        if ((j & 1) && j < n_loop) iter(j++, IC<1>{}, IC<1>{});
+        j = max(j, n_unm);
+        if (((j - j_lo) & 1) && j < n_loop) iter(j++, IC<1>{}, IC<1>{});
         for (; j < n_loop; j += 2) {
             iter(j, IC<0>{}, IC<1>{});
             if (j + 1 < n_loop) iter(j + 1, IC<1>{}, IC<1>{});
@@ -1486,17 +1520,18 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     FA_STAMP(s_loop_end);
     // ---- debug variant: every tile masked, not pipelined -----------------------------------
     if (n_loop < n_end) {
-        stage_v(n_loop);  // the pipeline fetched V one tile late; catch up before the first one
+        stage_v(n_loop, (n_loop - j_lo) & 1);  // the pipeline fetched V one tile late; catch up first
         dma_wait();
         __syncthreads();
     }
     for (int j = n_loop; j < n_end; ++j) {
+        const int sl = (j - j_lo) & 1;
         if (j + 1 < n_end) {
-            stage_k(j + 1);
-            stage_v(j + 1);
+            stage_k(j + 1, sl ^ 1);
+            stage_v(j + 1, sl ^ 1);
         }
-        const char *K = lds + KV0 + (j & 1) * T;
-        const char *V = lds + KV0 + (2 + (j & 1)) * T;
+        const char *K = lds + KV0 + sl * T;
+        const char *V = lds + KV0 + (2 + sl) * T;
         const int key0 = j * kBlockN;
         phase1(K, IC<0>{}, IC<0>{}, IC<0>{}, k_rsrc(j), k_rsrc(j));
         s_ready(S[0][0], S[0][1]);
@@ -1504,7 +1539,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         mask(S[0][0], S[0][1], mw + r, key0);
         mask(S[0][2], S[0][3], mw + 32 + r, key0);
         sm1_all(IC<0>{});
-        rescale(j == 0);
+        rescale(j == j_lo);
         sm2_all(IC<0>{});
         phase2(V, IC<0>{}, IC<0>{}, IC<0>{});
         dma_wait();
@@ -1515,7 +1550,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // Every wave is past this block's last barrier: the Q AGPRs and both K slots are free (the
     // drain reads only a V slot).
     char *const ob_c = ob;
-    const int mw_c = mw, sq_c = Sq;
+    const int mw_c = mw, sq_c = Sq, jlo_c = j_lo;
 #ifdef FA_STAMPS
     const uint32_t blk_c = xcd + 8 * kblk;
 #endif
@@ -1532,7 +1567,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         } else if (!rope_q) {
             load_q();
         }
-        stage_k(0);
+        stage_k(j_lo, 0);
         if (q_in_agpr) q_from_lds();
     }
     // drain the last pipelined tile: softmax half 2 and P.V
@@ -1541,8 +1576,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         sm2_all(PAR);
         phase2(lds + KV0 + (2 + c) * T, PAR, PAR, IC<0>{});
     };
-    if (n_loop > 0) {
-        if ((n_loop - 1) & 1) drain(IC<1>{}); else drain(IC<0>{});
+    if (n_loop > jlo_c) {  // (set_block above moved j_lo to the next block)
+        if ((n_loop - 1 - jlo_c) & 1) drain(IC<1>{}); else drain(IC<0>{});
     }
     FA_STAMP(s_pipe_end);
 
@@ -1615,12 +1650,14 @@ int launch_p8(const fa_fwd_params &p, hipStream_t stream);
 
 // ---- host launch of one instantiation -------------------------------------------------
 template <class DT, bool C, int kD, bool kExact>
-int launch_one(const fa_fwd_params &p, const int *cu_q, const int *cu_k, const RopeArgs &rope, hipStream_t stream) {
-    if (rope.cos && !kExact) return set_err(FA_ERR_UNSUPPORTED, "fused RoPE needs head dim 64 or 128");
+int launch_one(const fa_fwd_params &p, const int *cu_q, const int *cu_k, const PathArgs &xa, hipStream_t stream) {
+    if (xa.cos && !kExact) return set_err(FA_ERR_UNSUPPORTED, "fused RoPE needs head dim 64 or 128");
     const int64_t n_qtiles = (p.seqlen_q + kBlockM - 1) / kBlockM;
     const int64_t nwg = n_qtiles * p.num_heads_q * p.batch_size;
-    // varlen and fused RoPE run fa_fwd_w4 (w4slow under the debug variant); w8 / p8 have neither
-    const int variant = (cu_q || rope.cos) && (variant_from_env() == 1 || variant_from_env() == 3) ? 0 : variant_from_env();
+    // varlen, fused RoPE and the local window run fa_fwd_w4 (w4slow under the debug variant); w8 / p8
+    // have none of them
+    const bool w4_only = cu_q || xa.cos || xa.window_left >= 0;
+    const int variant = w4_only && (variant_from_env() == 1 || variant_from_env() == 3) ? 0 : variant_from_env();
     if (variant == 3) return launch_p8<DT, C, kD, kExact>(p, stream);
     if (variant == 1)
         hipLaunchKernelGGL((fa_fwd_w8<DT, C, kD, kExact>), dim3((uint32_t)nwg), dim3(kThreads), 0, stream, p,
@@ -1628,7 +1665,7 @@ int launch_one(const fa_fwd_params &p, const int *cu_q, const int *cu_k, const R
     else
         // persistent: about one workgroup per CU (the kernel walks the Q blocks itself)
         hipLaunchKernelGGL((fa_fwd_w4<DT, C, kD, kExact>), dim3((uint32_t)w4_grid(nwg)), dim3(256), 0, stream, p,
-                           (int)n_qtiles, variant == 2 ? 1 : 0, stamp_buffer(), cu_q, cu_k, rope);
+                           (int)n_qtiles, variant == 2 ? 1 : 0, stamp_buffer(), cu_q, cu_k, xa);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "HIP launch failed: %s", hipGetErrorString(e));
     set_last_path(variant == 1 ? kPathW8 : variant == 2 ? kPathW4Slow : kPathW4);

@@ -57,20 +57,25 @@ unsigned long long *stamp_buffer();
 // deals Q blocks to workgroups by bid mod 8). FA_W4_GRID=<n> overrides the cap (A/B runs, tests).
 int64_t w4_grid(int64_t nwg);
 
+// Optional parts of a prefill launch.
 // RoPE tables for the Q load (fa_fwd_gfx950_rope): cos / sin [.., Sq, D] of the q dtype, strides in
 // elements (row of query m of batch b: b * batch_stride + m * seq_stride; varlen: packed row *
 // seq_stride). cos == nullptr: no rotation.
-struct RopeArgs {
+// Local window (fa_fwd_gfx950_window): key n is visible to query m only if n >= m + Sk - Sq -
+// window_left (the sliding window of window_left + 1 keys ending at the bottom-right diagonal);
+// window_left < 0: none.
+struct PathArgs {
     const void *cos;
     const void *sin;
     int64_t batch_stride;
     int64_t seq_stride;
+    int window_left;
 };
 
 // launch one (dtype, causal, head-dim tile, exact head dim) instantiation on `stream`; cu_q / cu_k
 // (device, [B + 1] prefix sums of the per-sequence lengths) select the varlen layout, or nullptr
 template <class DT, bool C, int kD, bool kExact>
-int launch_one(const fa_fwd_params &p, const int *cu_q, const int *cu_k, const RopeArgs &rope, hipStream_t stream);
+int launch_one(const fa_fwd_params &p, const int *cu_q, const int *cu_k, const PathArgs &xa, hipStream_t stream);
 
 
 // ---- split-KV decode (fa_decode.hpp) -------------------------------------------------------------
@@ -141,7 +146,7 @@ int launch_decode(const fa_fwd_params &p, DecArgs a, void *ws, hipStream_t strea
     X(BF16, true, 128, false) X(BF16, true, 128, true)
 
 #define FA_DECLARE_EXTERN(DT, C, D, E)                                                  \
-    extern template int launch_one<DT, C, D, E>(const fa_fwd_params &, const int *, const int *, const RopeArgs &, \
+    extern template int launch_one<DT, C, D, E>(const fa_fwd_params &, const int *, const int *, const PathArgs &, \
                                                 hipStream_t);                                                 \
     extern template int launch_decode<DT, C, D, E>(const fa_fwd_params &, DecArgs, void *, hipStream_t);
 FA_FOR_EACH_INSTANCE(FA_DECLARE_EXTERN)

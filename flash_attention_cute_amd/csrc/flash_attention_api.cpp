@@ -113,8 +113,9 @@ torch::Tensor rope_apply(torch::Tensor &x, torch::Tensor &cos, torch::Tensor &si
     return out;
 }
 
-torch::Tensor flash_attention_fwd(torch::Tensor &q, torch::Tensor &k, torch::Tensor &v, float softmax_scale,
-                                  bool causal) {
+// window_left >= 0 (flash_attention_window_fwd, after its cut): the local-window entry, no pack
+torch::Tensor fwd_impl(torch::Tensor &q, torch::Tensor &k, torch::Tensor &v, float softmax_scale, bool causal,
+                       int64_t window_left) {
     // Check input shape (reference :21-37)
     TORCH_CHECK(q.dim() == 4 && k.dim() == 4 && v.dim() == 4, "q, k, v must be 4-D [batch, heads, seqlen, dim]");
     TORCH_CHECK(q.size(0) == k.size(0) && q.size(0) == v.size(0), "q, k, v must have the same batch size");
@@ -163,7 +164,7 @@ torch::Tensor flash_attention_fwd(torch::Tensor &q, torch::Tensor &k, torch::Ten
     // Decode q-head packing (reference :64-83): with one query row per head, the q-heads of one
     // kv group become the rows of a single (batch, kv-head) problem so one workgroup serves the
     // whole group from one K/V stream. Causal masking is dropped, as in the reference (:81).
-    const bool is_pack_head_q = seqlen_q == 1;
+    const bool is_pack_head_q = seqlen_q == 1 && window_left < 0;
     if (is_pack_head_q) {
         head_q = head_kv;
         seqlen_q = seqlen_q * head_q_per_group;
@@ -209,6 +210,12 @@ torch::Tensor flash_attention_fwd(torch::Tensor &q, torch::Tensor &k, torch::Ten
 
     const int dtype = qx.scalar_type() == torch::kHalf ? FA_DTYPE_F16 : FA_DTYPE_BF16;
     void *stream = c10::hip::getCurrentHIPStream(qx.device().index()).stream();
+    if (window_left >= 0) {
+        const int rc = fa_fwd_gfx950_window(&params, dtype, causal ? 1 : 0, window_left, stream);
+        TORCH_CHECK(rc == FA_OK, "fa_fwd_gfx950_window failed (code ", rc, "): ", fa_last_error());
+        if (o.sizes() != q.sizes()) o = o.reshape(q.sizes());
+        return o;
+    }
     // split-KV decode (few rows per kv-head) wants fp32 scratch for its partials: taken from
     // torch's caching allocator on the current stream, so it is graph-capture safe and reused
     const int64_t ws_bytes = fa_fwd_gfx950_workspace_size(&params, dtype, causal ? 1 : 0);
@@ -226,6 +233,28 @@ torch::Tensor flash_attention_fwd(torch::Tensor &q, torch::Tensor &k, torch::Ten
     }
     if (o.sizes() != q.sizes()) o = o.reshape(q.sizes());
     return o;
+}
+
+torch::Tensor flash_attention_fwd(torch::Tensor &q, torch::Tensor &k, torch::Tensor &v, float softmax_scale,
+                                  bool causal) {
+    return fwd_impl(q, k, v, softmax_scale, causal, -1);
+}
+
+// Local (sliding-window) attention, include/fa_gfx950.h fa_fwd_gfx950_window: key n visible to query
+// m iff n >= m + Sk - Sq - window_left (and, causal, n <= m + Sk - Sq). The keys left of every row's
+// window are cut off here as views of k / v; when the window masks nothing more (decode: Sq == 1)
+// the plain forward runs on the rest (q-head pack and split-KV decode included).
+torch::Tensor flash_attention_window_fwd(torch::Tensor &q, torch::Tensor &k, torch::Tensor &v, int64_t window_left,
+                                         float softmax_scale, bool causal) {
+    TORCH_CHECK(window_left >= 0, "window_left must be >= 0");
+    TORCH_CHECK(q.dim() == 4 && k.dim() == 4 && v.dim() == 4, "q, k, v must be 4-D [batch, heads, seqlen, dim]");
+    TORCH_CHECK(k.size(2) == v.size(2), "k, v must have the same sequence length");
+    const int64_t sq = q.size(2), sk = k.size(2);
+    const int64_t cut = sk - sq - window_left;
+    torch::Tensor kc = cut > 0 ? k.narrow(2, cut, sk - cut) : k;
+    torch::Tensor vc = cut > 0 ? v.narrow(2, cut, sk - cut) : v;
+    if (kc.size(2) - 1 <= window_left) return fwd_impl(q, kc, vc, softmax_scale, causal, -1);
+    return fwd_impl(q, kc, vc, softmax_scale, causal, window_left);
 }
 
 // Attention with RoPE applied to q inside the kernel's Q load (fa_fwd_gfx950_rope); k is already
@@ -395,6 +424,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           "FlashAttention-2 forward over packed variable-length sequences (cu_seqlens), gfx950");
     m.def("flash_attention_rope_fwd", &flash_attention::flash_attention_rope_fwd,
           "FlashAttention-2 forward with rotate-half RoPE applied to q in the kernel's Q load, gfx950");
+    m.def("flash_attention_window_fwd", &flash_attention::flash_attention_window_fwd,
+          "FlashAttention-2 forward with a local (sliding) window of window_left + 1 keys, gfx950");
     m.def("rope_apply", &flash_attention::rope_apply, "rotate-half RoPE, one HIP pass (gfx950)");
     m.def("abi_version", []() { return fa_abi_version(); });
 }

@@ -228,3 +228,68 @@ def flash_attn_rope_func(q, k, v, cos, sin, softmax_scale=None, causal=False):
     attention kernel's Q load; k must already be rotated (``apply_rope``)."""
     softmax_scale = (q.size(-1) ** -0.5) if softmax_scale is None else softmax_scale
     return torch.ops.flash_attention.rope_forward(q, k, v, cos, sin, softmax_scale, causal)
+
+
+# ---------------------------------------------------------------------------------------------
+# Local (sliding-window) attention -- the reference computes the Qwen2 sliding window and then
+# ignores it (reference models/rope_attn_fwd.py:95-101); include/fa_gfx950.h fa_fwd_gfx950_window.
+# ---------------------------------------------------------------------------------------------
+def _window_mask(sq: int, sk: int, window_left: int, causal: bool, device) -> torch.Tensor:
+    """[sq, sk] bool, True = visible: key n is visible to query m iff n >= m + sk - sq - window_left
+    and, with causal, n <= m + sk - sq (transformers' sliding_window_causal_mask_function with
+    sliding_window = window_left + 1, bottom-right aligned as the kernel's causal mask)."""
+    m = torch.arange(sq, device=device)[:, None]
+    n = torch.arange(sk, device=device)[None, :]
+    vis = n >= m + (sk - sq) - window_left
+    if causal:
+        vis = vis & (n <= m + (sk - sq))
+    return vis
+
+
+@torch.library.custom_op("flash_attention::window_forward", mutates_args=())
+def flash_attention_window_forward(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, window_left: int,
+                                   softmax_scale: float = None, causal: bool = False) -> torch.Tensor:
+    # q: [B, Hq, Sq, D]; k, v: [B, Hkv, Sk, D]. Non-GPU default: torch SDPA under the window mask
+    # (GQA expanded; rows that see no key are 0, as on the GPU).
+    warnings.warn("Flash Attention only support cuda now, fallback to pytorch implementation.", stacklevel=2)
+    mask = _window_mask(q.size(2), k.size(2), window_left, causal, q.device)
+    o = torch.nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=mask, scale=softmax_scale,
+                                                         enable_gqa=True)
+    return o.masked_fill(~mask.any(dim=1)[None, None, :, None], 0)
+
+
+@torch.library.register_kernel("flash_attention::window_forward", "cuda")
+def flash_attention_window_forward_cuda(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, window_left: int,
+                                        softmax_scale: float = None, causal: bool = False) -> torch.Tensor:
+    if flash_attention_cuda is None:
+        raise RuntimeError(f"gfx950 flash attention extension is not available: {_load_error!r}")
+    if window_left < 0:
+        raise ValueError(f"window_left must be >= 0 (got {window_left})")
+    head_dim = q.size(3)
+    need_padding = head_dim % 8 != 0
+    if need_padding:
+        pad = [0, 8 - head_dim % 8]
+        q = torch.nn.functional.pad(q, pad)
+        k = torch.nn.functional.pad(k, pad)
+        v = torch.nn.functional.pad(v, pad)
+    q = q.contiguous() if q.stride(3) != 1 else q
+    k = k.contiguous() if k.stride(3) != 1 else k
+    v = v.contiguous() if v.stride(3) != 1 else v
+    attn = flash_attention_cuda.flash_attention_window_fwd(q, k, v, int(window_left), softmax_scale, causal)
+    if need_padding:
+        attn = attn[:, :, :, :head_dim]
+    return attn
+
+
+@torch.library.register_fake("flash_attention::window_forward")
+def flash_attention_window_forward_fake(q, k, v, window_left, softmax_scale=None, causal=False):
+    return torch.empty_like(q)
+
+
+def flash_attn_window_func(q, k, v, window_left, softmax_scale=None, causal=False):
+    """``flash_attn_func`` where query m sees only keys n >= m + Sk - Sq - window_left: a sliding
+    window of ``window_left + 1`` keys ending at the (bottom-right) diagonal with ``causal``.
+    transformers' ``sliding_window`` W is ``window_left = W - 1`` (flash-attn ``window_size=(W - 1,
+    -1)``)."""
+    softmax_scale = (q.size(-1) ** -0.5) if softmax_scale is None else softmax_scale
+    return torch.ops.flash_attention.window_forward(q, k, v, int(window_left), softmax_scale, causal)

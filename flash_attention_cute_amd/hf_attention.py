@@ -8,8 +8,8 @@ verified against the installed transformers fixed:
 
 1. ``self.config.use_sliding_window`` raised AttributeError on ``LlamaConfig``
    (reference models/rope_attn_fwd.py:97): read with ``getattr(..., False)``; a sliding window
-   that would actually cut the visible keys raises NotImplementedError instead of being ignored
-   (the kernel has no local-window mask);
+   that cuts the visible keys runs the local-window kernel (``flash_attn_window_func``,
+   window_left = sliding_window - 1) instead of being ignored as in the reference (:95-101);
 2. HF passes the cache as ``past_key_values=`` (plural) while the reference takes
    ``past_key_value`` (:71) and silently drops the cache on decode: both names are accepted;
 3. decode (Sq == 1) with ``is_causal=True`` must see every cached key: the GPU kernel's causal mask
@@ -28,7 +28,8 @@ from typing import Optional, Tuple
 import torch
 from torch import nn
 
-from .flash_attention import _bottom_right_causal, apply_rope, flash_attn_func, flash_attn_rope_func, flash_attn_varlen_func
+from .flash_attention import (_bottom_right_causal, _window_mask, apply_rope, flash_attn_func, flash_attn_rope_func,
+                              flash_attn_varlen_func, flash_attn_window_func)
 
 # On GPU tensors the patched forward rotates k with one HIP pass (apply_rope) and q inside the
 # attention kernel (flash_attn_rope_func) instead of the reference's elementwise torch ops
@@ -53,15 +54,16 @@ def apply_rotary_pos_emb(q, k, cos, sin, position_ids=None, unsqueeze_dim=1):
     return q * cos + rotate_half(q) * sin, k * cos + rotate_half(k) * sin
 
 
-def key_padding(attention_mask: Optional[torch.Tensor], sq: int, sk: int, causal: bool) -> Optional[torch.Tensor]:
+def key_padding(attention_mask: Optional[torch.Tensor], sq: int, sk: int, causal: bool,
+                window_left: Optional[int] = None) -> Optional[torch.Tensor]:
     """Lower an HF attention mask to per-token validity ``[B, Sk]`` (True = real token), or None when it
-    masks nothing beyond the plain causal mask.
+    masks nothing beyond the plain causal (and, with ``window_left``, sliding-window) mask.
 
     Accepted: a 2-D padding mask ``[B, Sk]`` (1 = real token), or the 4-D mask HF builds for SDPA /
     eager ``[B, 1, Sq, Sk]`` (bool, True = attend; or additive float, 0 = attend) that is exactly
-    "causal (bottom-right) AND key not padding" on every real query row. A query row is real iff
-    its own token (key position m + Sk - Sq) is. Any other mask (sliding / chunked / custom) raises
-    NotImplementedError instead of being silently ignored as in the reference
+    "causal (bottom-right) AND inside the window AND key not padding" on every real query row. A
+    query row is real iff its own token (key position m + Sk - Sq) is. Any other mask (chunked /
+    custom) raises NotImplementedError instead of being silently ignored as in the reference
     (models/rope_attn_fwd.py:40-64 drops ``attention_mask``).
     """
     if attention_mask is None:
@@ -79,10 +81,15 @@ def key_padding(attention_mask: Optional[torch.Tensor], sq: int, sk: int, causal
             raise NotImplementedError(f"flash_attention_cute_amd: 4-D attention_mask of shape {tuple(m.shape)} "
                                       f"(expected [B, 1, {sq}, {sk}])")
         m = m[:, 0] if m.dtype == torch.bool else (m[:, 0] == 0)
-        kv_valid = m.any(dim=1)
-        allowed = kv_valid[:, None, :]
-        if causal:
-            allowed = allowed & _bottom_right_causal(sq, sk, m.device)[None]
+        if window_left is not None:
+            shape = _window_mask(sq, sk, window_left, causal, m.device)
+        elif causal:
+            shape = _bottom_right_causal(sq, sk, m.device)
+        else:
+            shape = torch.ones(sq, sk, dtype=torch.bool, device=m.device)
+        # a key no row attends to is padding, unless the causal / window shape hides it from every row
+        kv_valid = m.any(dim=1) | ~shape.any(dim=0)[None]
+        allowed = kv_valid[:, None, :] & shape[None]
         q_valid = kv_valid[:, sk - sq:]
         if bool(((m != allowed) & q_valid[:, :, None]).any()):
             raise NotImplementedError("flash_attention_cute_amd: only causal + key-padding attention masks are "
@@ -128,16 +135,24 @@ def _flash_attention_forward(module: nn.Module, query: torch.Tensor, key: torch.
     if dropout:
         raise NotImplementedError("flash_attention_cute_amd: attention dropout is not supported (forward only)")
     sq, sk = query.shape[2], key.shape[2]
-    if sliding_window is not None and sk > sliding_window:
-        raise NotImplementedError(
-            f"flash_attention_cute_amd: sliding window {sliding_window} shorter than the {sk} visible keys")
     causal = bool(getattr(module, "is_causal", True)) and sq > 1
+    # a sliding window of W keys (transformers: key n visible to the query at position p iff
+    # p - W < n <= p) that cuts the visible keys: the local-window kernel, window_left = W - 1
+    window_left = sliding_window - 1 if sliding_window is not None and sk > sliding_window else None
     rope = kwargs.pop("rope_q", None)  # (cos, sin): q still to be rotated (fused path)
-    kv_valid = key_padding(attention_mask, sq, sk, causal)
+    kv_valid = key_padding(attention_mask, sq, sk, causal, window_left)
     if kv_valid is not None:
+        if window_left is not None:
+            raise NotImplementedError("flash_attention_cute_amd: a padding mask together with a sliding window "
+                                      f"({sliding_window}) is not supported")
         if rope is not None:
             query = apply_rope(query, *rope)
         return _varlen_attention(query, key, value, kv_valid, causal, scaling), None
+    if window_left is not None:
+        if rope is not None:
+            query = apply_rope(query, *rope)
+        attn_output = flash_attn_window_func(query, key, value, window_left, softmax_scale=scaling, causal=causal)
+        return attn_output.transpose(1, 2), None
     if rope is not None:
         attn_output = flash_attn_rope_func(query, key, value, *rope, causal=causal, softmax_scale=scaling)
     else:

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define FA_GFX950_ABI_VERSION 4
+#define FA_GFX950_ABI_VERSION 5
 
 /* Field order mirrors reference csrc/flash_attention.h:5-37. */
 typedef struct fa_fwd_params {
@@ -187,6 +187,18 @@ typedef struct fa_rope_fwd_params {
 } fa_rope_fwd_params;
 
 int fa_fwd_gfx950_rope(const fa_rope_fwd_params *params, int dtype, int causal, void *stream);
+
+/*
+ * Local (sliding-window) attention: as fa_fwd_gfx950, and key n is visible to query m only if
+ * n >= m + seqlen_kv - seqlen_q - window_left, i.e. each query sees at most the window_left + 1
+ * keys ending at its bottom-right diagonal (with causal; without it, every key from that one on).
+ * This is transformers' sliding_window (window_left = sliding_window - 1; flash-attn
+ * window_size = (window_left, -1)). The reference computes the Qwen2 sliding window and ignores it
+ * (reference models/rope_attn_fwd.py:95-101). Keys left of every row's window are cut off the
+ * problem; if the window then masks nothing more the call is fa_fwd_gfx950 on the rest (split-KV
+ * decode included), else the prefill kernel masks it. window_left < 0: no window.
+ */
+int fa_fwd_gfx950_window(const fa_fwd_params *params, int dtype, int causal, int64_t window_left, void *stream);
 
 /*
  * Standalone rotate-half RoPE, out = x * cos + rotate_half(x) * sin (same arithmetic as the fused

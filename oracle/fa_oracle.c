@@ -90,9 +90,15 @@ static inline float round_t(float x, int dtype) { return to_f(from_f(x, dtype), 
  * scale (log2(e) is folded in here, as the host API does). dtype 0 = fp16, 1 = bf16.
  * o32 (optional) receives the unrounded fp32 output. Returns 0, or -1 on invalid shapes.
  */
-int fa_oracle_fwd(const uint16_t *q, const uint16_t *k, const uint16_t *v, uint16_t *o, float *o32, int64_t B,
-                  int64_t Hq, int64_t Hkv, int64_t Sq, int64_t Sk, int64_t D, float softmax_scale, int causal,
-                  int dtype, int threads) {
+/*
+ * window_left >= 0: key n is also masked for query m when n < m + Sk - Sq - window_left (the local
+ * window of include/fa_gfx950.h fa_fwd_gfx950_window; the reference has no such mask, so this part
+ * follows transformers' sliding_window_causal_mask_function with sliding_window = window_left + 1).
+ * With Sq == 1 every packed q-head row is the one query at position Sk - 1.
+ */
+int fa_oracle_fwd_window(const uint16_t *q, const uint16_t *k, const uint16_t *v, uint16_t *o, float *o32,
+                         int64_t B, int64_t Hq, int64_t Hkv, int64_t Sq, int64_t Sk, int64_t D, float softmax_scale,
+                         int causal, int dtype, int threads, int64_t window_left) {
     if (B <= 0 || Hq <= 0 || Hkv <= 0 || Sq <= 0 || Sk <= 0 || D <= 0 || Hq % Hkv) return -1;
     const int64_t group = Hq / Hkv;
     const float s2 = (float)((double)softmax_scale * 1.4426950408889634);
@@ -153,7 +159,9 @@ int fa_oracle_fwd(const uint16_t *q, const uint16_t *k, const uint16_t *v, uint1
                     float mx = -INFINITY;
                     for (int64_t c = 0; c < BN; ++c) {
                         float sv = -INFINITY;
-                        const int visible = c < nc && (!causal || c0 + c <= r0 + r + diag);
+                        int visible = c < nc && (!causal || c0 + c <= r0 + r + diag);
+                        if (window_left >= 0)
+                            visible = visible && c0 + c >= (Sq == 1 ? Sk - 1 : r0 + r + diag) - window_left;
                         if (visible) {
                             const float *kr = ks + c * D;
                             float a = 0.f;
@@ -200,6 +208,12 @@ int fa_oracle_fwd(const uint16_t *q, const uint16_t *k, const uint16_t *v, uint1
         free(acc);
     }
     return 0;
+}
+
+int fa_oracle_fwd(const uint16_t *q, const uint16_t *k, const uint16_t *v, uint16_t *o, float *o32, int64_t B,
+                  int64_t Hq, int64_t Hkv, int64_t Sq, int64_t Sk, int64_t D, float softmax_scale, int causal,
+                  int dtype, int threads) {
+    return fa_oracle_fwd_window(q, k, v, o, o32, B, Hq, Hkv, Sq, Sk, D, softmax_scale, causal, dtype, threads, -1);
 }
 
 int fa_oracle_max_threads(void) {

@@ -34,6 +34,8 @@ def _load():
         lib.fa_oracle_fwd.argtypes = [ctypes.c_void_p] * 5 + [i64] * 6 + [ctypes.c_float, ctypes.c_int,
                                                                          ctypes.c_int, ctypes.c_int]
         lib.fa_oracle_fwd.restype = ctypes.c_int
+        lib.fa_oracle_fwd_window.argtypes = lib.fa_oracle_fwd.argtypes + [i64]
+        lib.fa_oracle_fwd_window.restype = ctypes.c_int
         lib.fa_oracle_max_threads.restype = ctypes.c_int
         _lib = lib
     return _lib
@@ -43,7 +45,10 @@ def max_threads() -> int:
     return _load().fa_oracle_max_threads()
 
 
-def forward(q, k, v, softmax_scale: float, causal: bool, threads: int = 0, want_f32: bool = False):
+def forward(q, k, v, softmax_scale: float, causal: bool, threads: int = 0, want_f32: bool = False,
+            window_left: int = -1):
+    """window_left >= 0: the local window of fa_fwd_gfx950_window (key n visible to query m only if
+    n >= m + Sk - Sq - window_left)."""
     import torch
 
     lib = _load()
@@ -56,9 +61,9 @@ def forward(q, k, v, softmax_scale: float, causal: bool, threads: int = 0, want_
     hkv, sk = k.shape[1], k.shape[2]
     o = torch.empty_like(q)
     o32 = torch.empty(q.shape, dtype=torch.float32) if want_f32 else None
-    rc = lib.fa_oracle_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
-                           o32.data_ptr() if o32 is not None else None, b, hq, hkv, sq, sk, d,
-                           float(softmax_scale), int(bool(causal)), dtype, int(threads))
+    rc = lib.fa_oracle_fwd_window(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
+                                  o32.data_ptr() if o32 is not None else None, b, hq, hkv, sq, sk, d,
+                                  float(softmax_scale), int(bool(causal)), dtype, int(threads), int(window_left))
     if rc != 0:
         raise ValueError("fa_oracle_fwd: invalid shapes")
     return (o, o32) if want_f32 else o

@@ -42,7 +42,8 @@ def test_header_declares_the_boundary():
     assert set(declared_functions()) == {"fa_fwd_gfx950", "fa_fwd_gfx950_check", "fa_last_error", "fa_abi_version",
                                          "fa_fwd_gfx950_geometry", "fa_fwd_gfx950_ws",
                                          "fa_fwd_gfx950_workspace_size", "fa_fwd_gfx950_varlen",
-                                         "fa_fwd_gfx950_varlen_check", "fa_fwd_gfx950_rope", "fa_rope_gfx950"}
+                                         "fa_fwd_gfx950_varlen_check", "fa_fwd_gfx950_rope", "fa_rope_gfx950",
+                                         "fa_fwd_gfx950_window"}
 
 
 def test_every_declared_symbol_is_exported(lib):
@@ -82,7 +83,7 @@ def check(lib, p, dtype=0, causal=0):
 
 def test_abi_version(lib):
     lib.fa_abi_version.restype = ctypes.c_int
-    assert lib.fa_abi_version() == 4
+    assert lib.fa_abi_version() == 5
 
 
 def test_check_accepts_valid(lib):
@@ -118,6 +119,14 @@ def test_launch_entry_validates_before_touching_the_device(lib):
     lib.fa_fwd_gfx950.restype = ctypes.c_int
     p = good_params(headdim=100)
     assert lib.fa_fwd_gfx950(ctypes.byref(p), 0, 0, None) == FA_ERR_INVALID_ARGUMENT
+
+
+def test_window_entry_validates_before_touching_the_device(lib):
+    lib.fa_fwd_gfx950_window.restype = ctypes.c_int
+    lib.fa_fwd_gfx950_window.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p]
+    p = good_params(headdim=100)
+    assert lib.fa_fwd_gfx950_window(ctypes.byref(p), 0, 1, 63, None) == FA_ERR_INVALID_ARGUMENT
+    assert lib.fa_fwd_gfx950_window(None, 0, 1, 63, None) == FA_ERR_INVALID_ARGUMENT
 
 
 def test_geometry(lib):

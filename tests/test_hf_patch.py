@@ -126,13 +126,72 @@ def test_decode_step_sees_whole_cache_on_cpu():
     torch.testing.assert_close(got[:, -1], ref[:, -1], atol=2e-5, rtol=1e-4)
 
 
-def test_active_sliding_window_is_rejected_not_ignored():
-    cfg = tiny_qwen2()
+def window_mask4(b, s, pos, w):
+    """HF's 4-D SDPA mask [B, 1, s, pos + s] of a sliding-window causal layer (True = attend) for s new
+    tokens at positions pos.. (transformers sliding_window_causal_mask_function: p - w < n <= p)."""
+    p_ = torch.arange(pos, pos + s)[:, None]
+    n = torch.arange(pos + s)[None, :]
+    return ((n <= p_) & (n > p_ - w))[None, None].expand(b, 1, s, pos + s)
+
+
+def run_window_layer(cfg, dev, dtype, seqs, w, patch, seed=0):
+    """A Qwen2 sliding-window layer (use_sliding_window, window w) through a DynamicCache, with the 4-D
+    sliding-window mask HF builds for SDPA passed to both the patched and the unpatched forward."""
+    torch.manual_seed(seed)
+    layer = mq.Qwen2Attention(cfg, layer_idx=0).to(dev, dtype).eval()
+    rope = mq.Qwen2RotaryEmbedding(cfg).to(dev)
+    # a cache that keeps every key (no sliding-window truncation), so the mask spans pos + s keys and
+    # the window itself is what hides the old ones
+    cache = DynamicCache()
+    x = torch.randn(2, sum(seqs), cfg.hidden_size, device=dev, dtype=dtype)
+    outs, pos = [], 0
+    ctx = patched(mq.Qwen2Attention) if patch else _null()
+    with ctx, torch.no_grad(), warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for s in seqs:
+            pid = torch.arange(pos, pos + s, device=dev)[None].expand(2, -1)
+            mask = window_mask4(2, s, pos, w).to(dev)
+            o, _ = layer(x[:, pos:pos + s], position_embeddings=rope(x, pid), attention_mask=mask,
+                         past_key_values=cache, cache_position=pid[0])
+            outs.append(o)
+            pos += s
+    return torch.cat(outs, dim=1)
+
+
+def sliding_qwen2(w, **kw):
+    cfg = tiny_qwen2(**kw)
     cfg.use_sliding_window = True
-    cfg.sliding_window = 4
+    cfg.sliding_window = w
     cfg.max_window_layers = 0
-    with pytest.raises(NotImplementedError, match="sliding window"):
-        run_layer(mq.Qwen2Attention, cfg, "cpu", torch.float32, seqs=(6,), patch=True)
+    cfg.layer_types = ["sliding_attention"] * cfg.num_hidden_layers
+    return cfg
+
+
+def test_active_sliding_window_runs_the_window_op_not_ignored():
+    """Reference models/rope_attn_fwd.py:95-101 computes the window and ignores it; the patch runs the
+    local-window op: same output as unpatched HF under HF's own sliding-window mask (prefill longer
+    than the window, then decode steps past it)."""
+    cfg = sliding_qwen2(4)
+    ref = run_window_layer(cfg, "cpu", torch.float32, (9, 1, 1), 4, patch=False)
+    got = run_window_layer(cfg, "cpu", torch.float32, (9, 1, 1), 4, patch=True)
+    torch.testing.assert_close(got, ref, atol=2e-5, rtol=1e-4)
+    # the window matters here: plain causal attention over the same tokens differs
+    full = run_layer(mq.Qwen2Attention, tiny_qwen2(), "cpu", torch.float32, seqs=(9, 1, 1), patch=True)
+    assert not torch.allclose(full, got, atol=1e-3)
+
+
+def test_sliding_window_with_padding_is_rejected():
+    b, s, w = 2, 6, 3
+    mask = window_mask4(b, s, 0, w).clone()
+    mask[0, :, :, 0] = False  # key 0 of sequence 0 is padding
+    mask[0, :, 0, :] = False
+    with pytest.raises(NotImplementedError):
+        kv = hf_attention.key_padding(mask, s, s, True, w - 1)
+        if kv is not None:
+            raise NotImplementedError
+    assert hf_attention.key_padding(window_mask4(b, s, 0, w), s, s, True, w - 1) is None
+    with pytest.raises(NotImplementedError, match="only causal"):
+        hf_attention.key_padding(window_mask4(b, s, 0, w), s, s, True, None)  # a window the caller did not declare
 
 
 def test_patch_attn_entry_points_swap_forward():
@@ -183,3 +242,20 @@ def test_patched_llama_model_generates_same_tokens_as_hf(device):
             got = model(ids).logits.float()
     assert (got - ref).abs().max().item() < 5e-2
     assert (got.argmax(-1) == ref.argmax(-1)).float().mean().item() > 0.95
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_patch_sliding_window_layer_matches_hf_on_gpu(device, dtype):
+    """Qwen2 sliding-window layer (window 128) on the GPU: a 300-token prefill (the window kernel)
+    and decode steps past the window (keys cut, decode kernel), against unpatched HF in fp32 under
+    HF's own sliding-window mask."""
+    from flash_attention_cute_amd import _debug
+
+    _debug.set_knobs()
+    cfg = sliding_qwen2(128, hq=8, hkv=2, d=128)
+    seqs = (300, 1, 1)
+    ref = run_window_layer(cfg, device, torch.float32, seqs, 128, patch=False)
+    got = run_window_layer(cfg, device, dtype, seqs, 128, patch=True)
+    tol = 2e-2 if dtype == torch.bfloat16 else 4e-3
+    torch.testing.assert_close(got.float(), ref, atol=tol, rtol=0)
