@@ -205,15 +205,19 @@ int check_varlen(const fa_varlen_params *v, int dtype, int causal) {
     return check_params(&p, dtype, causal);
 }
 
-int dispatch_varlen(const fa_varlen_params *v, int dtype, int causal, void *stream) {
+// window_left >= 0: the local window per sequence (the kernel starts each Q block at its first
+// visible tile; no host cut, the sequence bounds live on the device)
+int dispatch_varlen(const fa_varlen_params *v, int dtype, int causal, void *stream, int64_t window_left = -1) {
     g_last_path = fa::kPathNone;
     const int rc = check_varlen(v, dtype, causal);
     if (rc != FA_OK) return rc;
     hipStream_t s = (hipStream_t)stream;
     const int *cq = v->cu_seqlens_q, *ck = v->cu_seqlens_k;
+    // a window at least as long as every sequence hides nothing (seqlen_kv is the maximum)
+    const fa::PathArgs xa{nullptr, nullptr, 0, 0, window_left < v->base.seqlen_kv ? (int)window_left : -1};
     if (dtype == FA_DTYPE_F16)
-        return causal ? launch<fa::F16, true>(v->base, s, cq, ck) : launch<fa::F16, false>(v->base, s, cq, ck);
-    return causal ? launch<fa::BF16, true>(v->base, s, cq, ck) : launch<fa::BF16, false>(v->base, s, cq, ck);
+        return causal ? launch<fa::F16, true>(v->base, s, cq, ck, xa) : launch<fa::F16, false>(v->base, s, cq, ck, xa);
+    return causal ? launch<fa::BF16, true>(v->base, s, cq, ck, xa) : launch<fa::BF16, false>(v->base, s, cq, ck, xa);
 }
 
 int dispatch_rope(const fa_rope_fwd_params *r, int dtype, int causal, void *stream) {
@@ -274,6 +278,11 @@ extern "C" int fa_fwd_gfx950_rope(const fa_rope_fwd_params *params, int dtype, i
 
 extern "C" int fa_fwd_gfx950_varlen(const fa_varlen_params *params, int dtype, int causal, void *stream) {
     return dispatch_varlen(params, dtype, causal, stream);
+}
+
+extern "C" int fa_fwd_gfx950_varlen_window(const fa_varlen_params *params, int dtype, int causal,
+                                           int64_t window_left, void *stream) {
+    return dispatch_varlen(params, dtype, causal, stream, window_left);
 }
 
 extern "C" int fa_fwd_gfx950_varlen_check(const fa_varlen_params *params, int dtype, int causal) {

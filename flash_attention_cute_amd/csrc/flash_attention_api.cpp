@@ -339,7 +339,7 @@ torch::Tensor flash_attention_rope_fwd(torch::Tensor &q, torch::Tensor &k, torch
 torch::Tensor flash_attention_varlen_fwd(torch::Tensor &q, torch::Tensor &k, torch::Tensor &v,
                                          torch::Tensor &cu_seqlens_q, torch::Tensor &cu_seqlens_k,
                                          int64_t max_seqlen_q, int64_t max_seqlen_k, float softmax_scale,
-                                         bool causal) {
+                                         bool causal, int64_t window_left) {
     TORCH_CHECK(q.dim() == 3 && k.dim() == 3 && v.dim() == 3, "varlen q, k, v must be 3-D [total, heads, dim]");
     TORCH_CHECK(k.size(0) == v.size(0), "k, v must have the same number of rows");
     TORCH_CHECK(k.size(1) == v.size(1), "k, v must have the same number of heads");
@@ -410,7 +410,8 @@ torch::Tensor flash_attention_varlen_fwd(torch::Tensor &q, torch::Tensor &k, tor
 
     const int dtype = qx.scalar_type() == torch::kHalf ? FA_DTYPE_F16 : FA_DTYPE_BF16;
     void *stream = c10::hip::getCurrentHIPStream(qx.device().index()).stream();
-    const int rc = fa_fwd_gfx950_varlen(&vp, dtype, causal ? 1 : 0, stream);
+    const int rc = window_left >= 0 ? fa_fwd_gfx950_varlen_window(&vp, dtype, causal ? 1 : 0, window_left, stream)
+                                    : fa_fwd_gfx950_varlen(&vp, dtype, causal ? 1 : 0, stream);
     TORCH_CHECK(rc == FA_OK, "fa_fwd_gfx950_varlen failed (code ", rc, "): ", fa_last_error());
     return o;
 }

@@ -93,10 +93,11 @@ def _bottom_right_causal(sq: int, sk: int, device) -> torch.Tensor:
 @torch.library.custom_op("flash_attention::varlen_forward", mutates_args=())
 def flash_attention_varlen_forward(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_seqlens_q: torch.Tensor,
                                    cu_seqlens_k: torch.Tensor, max_seqlen_q: int, max_seqlen_k: int,
-                                   softmax_scale: float = None, causal: bool = False) -> torch.Tensor:
+                                   softmax_scale: float = None, causal: bool = False,
+                                   window_left: int = -1) -> torch.Tensor:
     # q: [total_q, n_heads, d]; k, v: [total_k, n_heads_kv, d]; cu_seqlens_*: int32 [batch_size + 1].
     # Non-GPU default: per-sequence torch SDPA with the kernel's semantics (bottom-right causal,
-    # GQA, rows that see no key are 0).
+    # GQA, rows that see no key are 0; window_left >= 0: the local window per sequence).
     warnings.warn("Flash Attention only support cuda now, fallback to pytorch implementation.", stacklevel=2)
     out = torch.zeros_like(q)
     cq, ck = cu_seqlens_q.tolist(), cu_seqlens_k.tolist()
@@ -105,10 +106,13 @@ def flash_attention_varlen_forward(q: torch.Tensor, k: torch.Tensor, v: torch.Te
         if q1 == q0 or k1 == k0:
             continue
         qs, ks, vs = (t.transpose(0, 1).unsqueeze(0) for t in (q[q0:q1], k[k0:k1], v[k0:k1]))
-        mask = _bottom_right_causal(q1 - q0, k1 - k0, q.device) if causal else None
+        if window_left >= 0:
+            mask = _window_mask(q1 - q0, k1 - k0, window_left, causal, q.device)
+        else:
+            mask = _bottom_right_causal(q1 - q0, k1 - k0, q.device) if causal else None
         o = torch.nn.functional.scaled_dot_product_attention(qs, ks, vs, attn_mask=mask, scale=softmax_scale,
                                                              enable_gqa=True)
-        if causal:  # rows with no visible key (Sq_b > Sk_b) are 0, as on the GPU
+        if mask is not None:  # rows with no visible key (Sq_b > Sk_b) are 0, as on the GPU
             o = o.masked_fill(~mask.any(dim=1)[None, None, :, None], 0)
         out[q0:q1] = o[0].transpose(0, 1)
     return out
@@ -118,7 +122,7 @@ def flash_attention_varlen_forward(q: torch.Tensor, k: torch.Tensor, v: torch.Te
 def flash_attention_varlen_forward_cuda(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
                                         cu_seqlens_q: torch.Tensor, cu_seqlens_k: torch.Tensor, max_seqlen_q: int,
                                         max_seqlen_k: int, softmax_scale: float = None,
-                                        causal: bool = False) -> torch.Tensor:
+                                        causal: bool = False, window_left: int = -1) -> torch.Tensor:
     if flash_attention_cuda is None:
         raise RuntimeError(f"gfx950 flash attention extension is not available: {_load_error!r}")
     head_dim = q.size(2)
@@ -132,7 +136,7 @@ def flash_attention_varlen_forward_cuda(q: torch.Tensor, k: torch.Tensor, v: tor
     k = k.contiguous() if k.stride(2) != 1 else k
     v = v.contiguous() if v.stride(2) != 1 else v
     attn = flash_attention_cuda.flash_attention_varlen_fwd(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q,
-                                                           max_seqlen_k, softmax_scale, causal)
+                                                           max_seqlen_k, softmax_scale, causal, int(window_left))
     if need_padding:
         attn = attn[:, :, :head_dim]
     return attn
@@ -140,18 +144,19 @@ def flash_attention_varlen_forward_cuda(q: torch.Tensor, k: torch.Tensor, v: tor
 
 @torch.library.register_fake("flash_attention::varlen_forward")
 def flash_attention_varlen_forward_fake(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k,
-                                        softmax_scale=None, causal=False):
+                                        softmax_scale=None, causal=False, window_left=-1):
     return torch.empty_like(q)
 
 
 def flash_attn_varlen_func(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, softmax_scale=None,
-                           causal=False):
+                           causal=False, window_left=-1):
     """Attention over packed sequences: q [total_q, Hq, D], k/v [total_k, Hkv, D]; sequence b owns rows
     [cu_seqlens_q[b], cu_seqlens_q[b+1]) of q and [cu_seqlens_k[b], cu_seqlens_k[b+1]) of k/v
-    (int32, on q's device). ``max_seqlen_q`` / ``max_seqlen_k`` must be the true maxima."""
+    (int32, on q's device). ``max_seqlen_q`` / ``max_seqlen_k`` must be the true maxima.
+    ``window_left >= 0``: the local window of ``flash_attn_window_func`` within each sequence."""
     softmax_scale = (q.size(-1) ** -0.5) if softmax_scale is None else softmax_scale
     return torch.ops.flash_attention.varlen_forward(q, k, v, cu_seqlens_q, cu_seqlens_k, int(max_seqlen_q),
-                                                    int(max_seqlen_k), softmax_scale, causal)
+                                                    int(max_seqlen_k), softmax_scale, causal, int(window_left))
 
 
 # ---------------------------------------------------------------------------------------------

@@ -87,19 +87,34 @@ def key_padding(attention_mask: Optional[torch.Tensor], sq: int, sk: int, causal
             shape = _bottom_right_causal(sq, sk, m.device)
         else:
             shape = torch.ones(sq, sk, dtype=torch.bool, device=m.device)
-        # a key no row attends to is padding, unless the causal / window shape hides it from every row
-        kv_valid = m.any(dim=1) | ~shape.any(dim=0)[None]
+        # a key no row attends to is padding; the keys the causal / window shape hides from every row
+        # (the window's prefix) cannot be told apart and are dropped with it: no row sees them
+        kv_valid = m.any(dim=1)
         allowed = kv_valid[:, None, :] & shape[None]
         q_valid = kv_valid[:, sk - sq:]
         if bool(((m != allowed) & q_valid[:, :, None]).any()):
             raise NotImplementedError("flash_attention_cute_amd: only causal + key-padding attention masks are "
                                       "supported (this mask masks other scores)")
+        if bool((kv_valid | ~shape.any(dim=0)[None]).all()):
+            return None  # no padding: the shape alone (the dense causal / window kernels)
     else:
         raise NotImplementedError(f"flash_attention_cute_amd: attention_mask with {m.dim()} dims")
-    return None if bool(kv_valid.all()) else kv_valid
+    if bool(kv_valid.all()):
+        return None
+    if window_left is not None:
+        # HF places the window on cache indices, the varlen kernel on the packed real tokens: the two
+        # agree when each sequence's real tokens are one contiguous run (left or right padding)
+        cnt = kv_valid.sum(1)
+        idx = torch.arange(sk, device=kv_valid.device)[None]
+        first = torch.where(kv_valid, idx, sk).amin(1)
+        last = torch.where(kv_valid, idx, -1).amax(1)
+        if bool(((last - first + 1 != cnt) & (cnt > 0)).any()):
+            raise NotImplementedError("flash_attention_cute_amd: a sliding window over padding that is not one "
+                                      "contiguous run per sequence")
+    return kv_valid
 
 
-def _varlen_attention(query, key, value, kv_valid, causal, scaling):
+def _varlen_attention(query, key, value, kv_valid, causal, scaling, window_left=-1):
     """Padded batch -> packed sequences -> ``flash_attn_varlen_func`` -> padded [B, Sq, Hq, D] (padding
     rows 0). q/k/v are [B, H, S, D] views; the valid query rows are the last Sq token positions."""
     b, hq, sq, d = query.shape
@@ -115,7 +130,7 @@ def _varlen_attention(query, key, value, kv_valid, causal, scaling):
     kp = key.transpose(1, 2).reshape(b * sk, hkv, d).index_select(0, idx_k)
     vp = value.transpose(1, 2).reshape(b * sk, hkv, d).index_select(0, idx_k)
     o = flash_attn_varlen_func(qp, kp, vp, cu_q, cu_k, int(lens_q.max()), int(lens_k.max()), softmax_scale=scaling,
-                               causal=causal)
+                               causal=causal, window_left=window_left)
     out = query.new_zeros(b * sq, hq, d)
     out.index_copy_(0, idx_q, o)
     return out.view(b, sq, hq, d)
@@ -142,12 +157,10 @@ def _flash_attention_forward(module: nn.Module, query: torch.Tensor, key: torch.
     rope = kwargs.pop("rope_q", None)  # (cos, sin): q still to be rotated (fused path)
     kv_valid = key_padding(attention_mask, sq, sk, causal, window_left)
     if kv_valid is not None:
-        if window_left is not None:
-            raise NotImplementedError("flash_attention_cute_amd: a padding mask together with a sliding window "
-                                      f"({sliding_window}) is not supported")
         if rope is not None:
             query = apply_rope(query, *rope)
-        return _varlen_attention(query, key, value, kv_valid, causal, scaling), None
+        return _varlen_attention(query, key, value, kv_valid, causal, scaling,
+                                 -1 if window_left is None else window_left), None
     if window_left is not None:
         if rope is not None:
             query = apply_rope(query, *rope)

@@ -165,6 +165,11 @@ typedef struct fa_varlen_params {
 
 int fa_fwd_gfx950_varlen(const fa_varlen_params *params, int dtype, int causal, void *stream);
 
+/* The varlen forward with the local window of fa_fwd_gfx950_window applied per sequence (key n of
+ * sequence b visible to its query m only if n >= m + Sk_b - Sq_b - window_left; < 0: none). */
+int fa_fwd_gfx950_varlen_window(const fa_varlen_params *params, int dtype, int causal, int64_t window_left,
+                                void *stream);
+
 /* Host-only validation of the varlen parameters (the device arrays are not read). */
 int fa_fwd_gfx950_varlen_check(const fa_varlen_params *params, int dtype, int causal);
 

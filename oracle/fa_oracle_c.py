@@ -73,7 +73,8 @@ if __name__ == "__main__":
     print(build(force=bool(os.environ.get("FORCE"))))
 
 
-def forward_varlen(q, k, v, cu_seqlens_q, cu_seqlens_k, softmax_scale: float, causal: bool, threads: int = 0):
+def forward_varlen(q, k, v, cu_seqlens_q, cu_seqlens_k, softmax_scale: float, causal: bool, threads: int = 0,
+                   window_left: int = -1):
     """Oracle of the varlen entry (include/fa_gfx950.h fa_fwd_gfx950_varlen): packed q [total_q, Hq, D],
     k/v [total_k, Hkv, D]; each sequence is the dense forward above on its own rows (bottom-right
     causal per sequence); a sequence without keys gives 0 rows."""
@@ -88,5 +89,6 @@ def forward_varlen(q, k, v, cu_seqlens_q, cu_seqlens_k, softmax_scale: float, ca
         if q1 == q0 or k1 == k0:
             continue
         qs, ks, vs = (t.transpose(0, 1).unsqueeze(0) for t in (q[q0:q1], k[k0:k1], v[k0:k1]))
-        out[q0:q1] = forward(qs, ks, vs, softmax_scale, causal, threads=threads)[0].transpose(0, 1)
+        out[q0:q1] = forward(qs, ks, vs, softmax_scale, causal, threads=threads,
+                             window_left=window_left)[0].transpose(0, 1)
     return out

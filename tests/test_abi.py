@@ -43,7 +43,7 @@ def test_header_declares_the_boundary():
                                          "fa_fwd_gfx950_geometry", "fa_fwd_gfx950_ws",
                                          "fa_fwd_gfx950_workspace_size", "fa_fwd_gfx950_varlen",
                                          "fa_fwd_gfx950_varlen_check", "fa_fwd_gfx950_rope", "fa_rope_gfx950",
-                                         "fa_fwd_gfx950_window"}
+                                         "fa_fwd_gfx950_window", "fa_fwd_gfx950_varlen_window"}
 
 
 def test_every_declared_symbol_is_exported(lib):

@@ -132,3 +132,67 @@ def test_window_qwen2_7b_dims_sampled_heads(device):
         hk = h // 7
         _check(out[:, h:h + 1], q[:, h:h + 1], k[:, hk:hk + 1], v[:, hk:hk + 1], 128 ** -0.5, True, 4095,
                torch.bfloat16)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16], ids=["f16", "bf16"])
+@pytest.mark.parametrize("causal", [True, False], ids=["causal", "full"])
+@pytest.mark.parametrize("wl", [0, 40, 200])
+def test_varlen_window_matches_oracle(device, wl, causal, dtype):
+    """The window per sequence of a packed batch (fa_fwd_gfx950_varlen_window): ragged, empty and
+    Sq != Sk sequences against the per-sequence oracle window."""
+    from flash_attention_cute_amd import _debug
+    from flash_attention_cute_amd import flash_attn_varlen_func
+    from tests.test_varlen import CASES as VCASES
+    from tests.test_varlen import pack
+
+    _debug.set_knobs()
+    for ci, case in enumerate(VCASES):
+        q, k, v, cu_q, cu_k, mq, mk = pack(case, dtype, 31 + ci + wl)
+        out = flash_attn_varlen_func(q.to(device), k.to(device), v.to(device), cu_q.to(device), cu_k.to(device), mq,
+                                     mk, causal=causal, window_left=wl)
+        torch.cuda.synchronize()
+        assert _debug.last_path() == "w4"
+        ref = OC.forward_varlen(q, k, v, cu_q, cu_k, case[2] ** -0.5, causal, window_left=wl).float()
+        got = out.float().cpu()
+        tol = TOL[dtype]
+        err = (got - ref).abs()
+        assert bool((err <= tol + tol * ref.abs()).all()), f"case {ci}: max err {err.max().item():.3e}"
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16], ids=["f16", "bf16"])
+def test_hf_sliding_window_padded_batch_on_gpu(device, dtype):
+    """Left-padded batch through a Qwen2 sliding-window layer (window 100) on the GPU: the varlen
+    kernel with the window per sequence; real tokens match unpatched HF in fp32."""
+    from transformers import DynamicCache
+    from transformers.models.qwen2 import modeling_qwen2 as mq
+
+    from flash_attention_cute_amd import _debug
+    from tests.test_hf_patch import _null, padded_window_mask4, patched, sliding_qwen2
+
+    _debug.set_knobs()
+    cfg = sliding_qwen2(100, hq=8, hkv=2, d=128)
+    lens, s = [300, 17, 250, 299], 300
+    valid = torch.zeros(4, s + 1, dtype=torch.bool, device=device)
+    for b, n in enumerate(lens):
+        valid[b, s - n:] = True
+    valid[:, s] = True
+    torch.manual_seed(0)
+    x = torch.randn(4, s + 1, cfg.hidden_size, device=device)
+    pid = (valid.long().cumsum(1) - 1).clamp(min=0)
+    outs = {}
+    for patch, dt in ((False, torch.float32), (True, dtype)):
+        torch.manual_seed(1)
+        layer = mq.Qwen2Attention(cfg, layer_idx=0).to(device, dt).eval()
+        rope = mq.Qwen2RotaryEmbedding(cfg).to(device)
+        cache = DynamicCache()
+        xx = x.to(dt)
+        with torch.no_grad(), (patched(mq.Qwen2Attention) if patch else _null()):
+            a, _ = layer(xx[:, :s], position_embeddings=rope(xx, pid[:, :s]),
+                         attention_mask=padded_window_mask4(valid, s, 0, 100), past_key_values=cache)
+            d, _ = layer(xx[:, s:], position_embeddings=rope(xx, pid[:, s:]),
+                         attention_mask=padded_window_mask4(valid, 1, s, 100), past_key_values=cache)
+        outs[patch] = (a.float(), d.float())
+    tol = 2e-2 if dtype == torch.bfloat16 else 4e-3
+    real = valid[:, :s]
+    torch.testing.assert_close(outs[True][0][real], outs[False][0][real], atol=tol, rtol=0)
+    torch.testing.assert_close(outs[True][1], outs[False][1], atol=tol, rtol=0)

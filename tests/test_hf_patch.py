@@ -180,18 +180,50 @@ def test_active_sliding_window_runs_the_window_op_not_ignored():
     assert not torch.allclose(full, got, atol=1e-3)
 
 
-def test_sliding_window_with_padding_is_rejected():
-    b, s, w = 2, 6, 3
-    mask = window_mask4(b, s, 0, w).clone()
-    mask[0, :, :, 0] = False  # key 0 of sequence 0 is padding
-    mask[0, :, 0, :] = False
-    with pytest.raises(NotImplementedError):
-        kv = hf_attention.key_padding(mask, s, s, True, w - 1)
-        if kv is not None:
-            raise NotImplementedError
-    assert hf_attention.key_padding(window_mask4(b, s, 0, w), s, s, True, w - 1) is None
+def padded_window_mask4(valid, s, pos, w):
+    """HF's 4-D SDPA mask of a sliding-window layer over a padded batch: the window on cache indices
+    (p - w < n <= p) AND the key is a real token."""
+    return window_mask4(valid.shape[0], s, pos, w).to(valid.device) & valid[:, None, None, :pos + s]
+
+
+def test_sliding_window_over_a_padded_batch_on_cpu():
+    """Left-padded batch through a Qwen2 sliding-window layer (window 4): the patch lowers the mask to
+    the varlen op with the window per sequence; real tokens match unpatched HF (prefill + decode)."""
+    from flash_attention_cute_amd import hf_attention as hfa
+
+    cfg = sliding_qwen2(4, hq=4, hkv=2)
+    torch.manual_seed(0)
+    layer = mq.Qwen2Attention(cfg, layer_idx=0).eval()
+    rope = mq.Qwen2RotaryEmbedding(cfg)
+    lens, s = [9, 5, 7], 9
+    valid = torch.zeros(3, s + 1, dtype=torch.bool)
+    for b, n in enumerate(lens):
+        valid[b, s - n:] = True
+    valid[:, s] = True
+    x = torch.randn(3, s + 1, cfg.hidden_size)
+    pid = (valid.long().cumsum(1) - 1).clamp(min=0)
+    outs = {}
+    for patch in (False, True):
+        cache = DynamicCache()
+        with torch.no_grad(), warnings.catch_warnings(), (patched(mq.Qwen2Attention) if patch else _null()):
+            warnings.simplefilter("ignore")
+            a, _ = layer(x[:, :s], position_embeddings=rope(x, pid[:, :s]),
+                         attention_mask=padded_window_mask4(valid, s, 0, 4), past_key_values=cache)
+            d, _ = layer(x[:, s:], position_embeddings=rope(x, pid[:, s:]),
+                         attention_mask=padded_window_mask4(valid, 1, s, 4), past_key_values=cache)
+        outs[patch] = (a, d)
+    real = valid[:, :s]
+    torch.testing.assert_close(outs[True][0][real], outs[False][0][real], atol=2e-5, rtol=1e-4)
+    torch.testing.assert_close(outs[True][1], outs[False][1], atol=2e-5, rtol=1e-4)
+    # the lowering: padding found, the window accepted; a window the caller did not declare raises
+    assert torch.equal(hfa.key_padding(padded_window_mask4(valid, s, 0, 4), s, s, True, 3), valid[:, :s])
     with pytest.raises(NotImplementedError, match="only causal"):
-        hf_attention.key_padding(window_mask4(b, s, 0, w), s, s, True, None)  # a window the caller did not declare
+        hfa.key_padding(padded_window_mask4(valid, s, 0, 4), s, s, True, None)
+    # padding inside a sequence: cache-index and packed-token windows differ -> rejected
+    holes = valid.clone()
+    holes[0, 4] = False
+    with pytest.raises(NotImplementedError, match="contiguous"):
+        hfa.key_padding(padded_window_mask4(holes, s, 0, 4), s, s, True, 3)
 
 
 def test_patch_attn_entry_points_swap_forward():

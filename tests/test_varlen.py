@@ -97,7 +97,7 @@ def test_varlen_op_registration():
     sch = str(torch.ops.flash_attention.varlen_forward.default._schema)
     assert sch == ("flash_attention::varlen_forward(Tensor q, Tensor k, Tensor v, Tensor cu_seqlens_q, "
                    "Tensor cu_seqlens_k, SymInt max_seqlen_q, SymInt max_seqlen_k, float softmax_scale=None, "
-                   "bool causal=False) -> Tensor")
+                   "bool causal=False, SymInt window_left=-1) -> Tensor")
     q, k, v, cu_q, cu_k, mq, mk = pack(CASES[0], torch.float32, 1)
     with warnings.catch_warnings():
         warnings.simplefilter("ignore")
