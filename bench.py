@@ -6,7 +6,7 @@ Metric (BASELINE.json): attn fwd TFLOPS + %MFMA peak at (B,H,S,D) = (4,32,4096,1
 ``flash_attn_func`` (custom op -> C++ host API -> C-ABI -> HIP kernel) over one batch of
 synthetic N(0,1) q, k, v already resident in HBM.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|c5_layer|decode|...] [--strong]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|c5_layer|decode|window|...] [--strong]
 
 Multi-GPU (launched by torch.distributed.run, one process per GPU; attention tiles are independent,
 so there is no data-path collective -- SURVEY.md 8(e)). A gloo process group carries only the
@@ -64,6 +64,10 @@ CONFIGS = {
     # split over the keys (split-KV + combine)
     "decode_long": dict(workload="decode GQA bf16 B1 Hq32 Hkv8 Sq1 Sk131072 D128 (split-KV)", B=1, Hq=32, Hkv=8,
                         Sq=1, Sk=131072, D=128, dtype="bf16", causal=False),
+    # local (sliding-window) attention: each query sees the last W keys up to itself (Mistral-7B-style
+    # window of 4096 on Llama-3-8B attention dims, 32k-token prefill); flash_attn_window_func
+    "window": dict(workload="sliding window GQA bf16 B1 Hq32 Hkv8 S32768 W4096 D128 causal", B=1, Hq=32, Hkv=8,
+                   Sq=32768, Sk=32768, D=128, dtype="bf16", causal=True, W=4096),
 }
 
 
@@ -77,6 +81,9 @@ def metric_of(key: str, c) -> str:
 
 
 def flops(c) -> float:
+    if c.get("W"):  # visible (query, key) pairs under the causal window (Sq == Sk >= W)
+        w, s_ = c["W"], c["Sq"]
+        return 4.0 * c["B"] * c["Hq"] * c["D"] * (w * (w + 1) / 2 + (s_ - w) * w)
     f = 4.0 * c["B"] * c["Hq"] * c["Sq"] * c["Sk"] * c["D"]
     return f / 2 if c["causal"] else f
 
@@ -109,11 +116,16 @@ def cpu_baseline(q, k, v, c, target_s: float) -> dict:
     try:
         qf, kf, vf = (t[:nb].float().cpu() for t in (q, k, v))
         causal = c["causal"] and c["Sq"] > 1
-        torch.nn.functional.scaled_dot_product_attention(qf[:, :1], kf[:, :1], vf[:, :1], is_causal=causal)
+        kw = {"is_causal": causal}
+        if c.get("W"):  # the window as an explicit mask
+            from flash_attention_cute_amd.flash_attention import _window_mask
+
+            kw = {"attn_mask": _window_mask(c["Sq"], c["Sk"], c["W"] - 1, causal, "cpu")}
+        torch.nn.functional.scaled_dot_product_attention(qf[:, :1], kf[:, :1], vf[:, :1], **kw)
         nrep = 3
         t0 = time.perf_counter()
         for _ in range(nrep):
-            torch.nn.functional.scaled_dot_product_attention(qf, kf, vf, is_causal=causal, enable_gqa=True)
+            torch.nn.functional.scaled_dot_product_attention(qf, kf, vf, enable_gqa=True, **kw)
         t_sdpa = (time.perf_counter() - t0) / nrep
         f_s = flops(dict(c, B=nb))
         out = {"value": round(f_s / t_sdpa / 1e12, 6), "unit": "TFLOPS", "cores": torch.get_num_threads(),
@@ -170,15 +182,16 @@ def cpu_port(q, k, v, c, target_s: float, cores: int) -> dict:
 
     scale = c["D"] ** -0.5
     # calibrate on one kv group, then size the sample to about target_s seconds of CPU work
+    wl = c["W"] - 1 if c.get("W") else -1
     qs, ks, vs = sample(g)
     t0 = time.perf_counter()
-    OC.forward(qs, ks, vs, scale, c["causal"], threads=cores)
+    OC.forward(qs, ks, vs, scale, c["causal"], threads=cores, window_left=wl)
     t1 = max(time.perf_counter() - t0, 1e-3)
     nh = int(min(c["Hq"], max(g, (target_s / t1) * g)))
     nh = max(g, (nh // g) * g)
     qs, ks, vs = sample(nh)
     t0 = time.perf_counter()
-    OC.forward(qs, ks, vs, scale, c["causal"], threads=cores)
+    OC.forward(qs, ks, vs, scale, c["causal"], threads=cores, window_left=wl)
     t_port = time.perf_counter() - t0
     f_sample = flops(dict(c, B=1, Hq=nh))
     return {"value": round(f_sample / t_port / 1e12, 6), "unit": "TFLOPS", "cores": cores, "kind": "port",
@@ -306,7 +319,7 @@ def main() -> None:
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
 
-    from flash_attention_cute_amd import flash_attn_func
+    from flash_attention_cute_amd import flash_attn_func, flash_attn_window_func
 
     c = CONFIGS[args.config]
     dt = torch.float16 if c["dtype"] == "fp16" else torch.bfloat16
@@ -330,6 +343,8 @@ def main() -> None:
         rank_bytes = sum(algo_bytes(dict(c, B=r.b_end - r.b, Hq=(r.h1 - r.h0) * g, Hkv=r.h1 - r.h0)) for r in runs)
 
         def step():
+            if c.get("W"):
+                return [flash_attn_window_func(a, b_, v_, c["W"] - 1, causal=c["causal"]) for a, b_, v_ in views]
             return [flash_attn_func(a, b_, v_, causal=c["causal"]) for a, b_, v_ in views]
 
         extra["shard"] = {"units": f"{c['B'] * c['Hkv']} (batch, kv-head)", "rank0_runs": len(runs)}
@@ -341,6 +356,8 @@ def main() -> None:
         rank_flops, rank_bytes = flops(c), algo_bytes(c)
 
         def step():
+            if c.get("W"):
+                return flash_attn_window_func(q, k, v, c["W"] - 1, causal=c["causal"])
             return flash_attn_func(q, k, v, causal=c["causal"])
 
     if layer:
@@ -422,6 +439,7 @@ def main() -> None:
                 ("; random-init Llama-3-8B attention weights, no checkpoint" if layer else ""),
         "config": {"workload": c["workload"], "batch": c["B"], "heads_q": c["Hq"], "heads_kv": c["Hkv"],
                    "seqlen_q": c["Sq"], "seqlen_kv": c["Sk"], "headdim": c["D"], "causal": c["causal"],
+                   **({"window": c["W"]} if c.get("W") else {}),
                    "parallelism": (f"dp{n_gpus}: (batch, kv-head) units of one problem split over ranks, no collective"
                                    if args.strong else
                                    f"dp{n_gpus} (independent batch x head shard per GPU, no collective)")},

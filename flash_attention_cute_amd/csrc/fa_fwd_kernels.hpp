@@ -244,7 +244,8 @@ struct Work {
     int qtile, hq, b;
 };
 template <bool kCausal>
-__device__ __forceinline__ Work decode_work(const uint32_t nwg, const uint32_t bid, const int n_qtiles, const int Hq) {
+__device__ __forceinline__ Work decode_work(const uint32_t nwg, const uint32_t bid, const int n_qtiles, const int Hq,
+                                            const int g) {
     const uint32_t xcd = bid & 7, k = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
     const uint32_t start = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
     const uint32_t cnt = q8 + (xcd < r8 ? 1u : 0u);
@@ -252,7 +253,10 @@ __device__ __forceinline__ Work decode_work(const uint32_t nwg, const uint32_t b
     uint32_t t, bh;
     if (kCausal && start % nq == 0 && cnt % nq == 0) {
         const uint32_t nb = cnt / nq;  // heads of this XCD
+        // at least one GQA group: with many q-tiles (long sequences, local windows) the XCD's CUs
+        // then run neighbouring q-tiles of the g q-heads that share one K/V stream
         uint32_t hg = 64u / nq;
+        hg = hg < (uint32_t)g ? (uint32_t)g : hg;
         hg = hg < 1u ? 1u : (hg > nb ? nb : hg);
         while (nb % hg) --hg;
         const uint32_t grp = k / (hg * nq), kk = k % (hg * nq);
@@ -282,7 +286,7 @@ __global__ __launch_bounds__(kThreads) void fa_fwd_w8(const fa_fwd_params p, con
     const int h = lane >> 5;
 
     // ---- XCD-aware work decode ----------------------------------------------------------
-    const Work wk = decode_work<kCausal>(gridDim.x, blockIdx.x, n_qtiles, (int)p.num_heads_q);
+    const Work wk = decode_work<kCausal>(gridDim.x, blockIdx.x, n_qtiles, (int)p.num_heads_q, (int)p.head_q_per_group);
     const int hq = wk.hq, b = wk.b, qtile = wk.qtile;
     const int hkv = hq / (int)p.head_q_per_group;
 
@@ -900,7 +904,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             j_um = min((max(lo1, 0) + kBlockN - 1) / kBlockN, n_end);
         }
     };
-    set_block(decode_work<kCausal>(nwg, xcd + 8 * kblk, n_qtiles, (int)p.num_heads_q));
+    set_block(decode_work<kCausal>(nwg, xcd + 8 * kblk, n_qtiles, (int)p.num_heads_q, (int)p.head_q_per_group));
 
     // ---- Q: this wave's 64 rows, B-operand fragments straight from HBM into AGPRs ----------
     // lane (h, r) of block X holds Q[mw + 32X + r][16*ks + 8*h + 0..7]; rows >= Sq read as 0.
@@ -992,7 +996,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         qn = 0;
         qnt = 0;
         if (kn < cnt) {
-            wk_next = decode_work<kCausal>(nwg, xcd + 8 * kn, n_qtiles, (int)p.num_heads_q);
+            wk_next = decode_work<kCausal>(nwg, xcd + 8 * kn, n_qtiles, (int)p.num_heads_q, (int)p.head_q_per_group);
             if (kQL && !rope_q) {
                 qnr = q_rsrc_of(wk_next);
                 qnt = NQP;
@@ -1001,7 +1005,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     };
     if (!rope_q) {
         if constexpr (kQL != 0) {
-            const rsrc_t qr0 = q_rsrc_of(decode_work<kCausal>(nwg, xcd + 8 * kblk, n_qtiles, (int)p.num_heads_q));
+            const rsrc_t qr0 = q_rsrc_of(decode_work<kCausal>(nwg, xcd + 8 * kblk, n_qtiles, (int)p.num_heads_q, (int)p.head_q_per_group));
             static_for<NQP>([&](auto N) { q_piece(qr0, decltype(N)::value); });
         } else {
             load_q();

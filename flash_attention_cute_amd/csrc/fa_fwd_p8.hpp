@@ -122,7 +122,7 @@ __global__ __launch_bounds__(512, 1) void fa_fwd_p8(const fa_fwd_params p, const
     char *ob;
     int m0, mw, n_end, n_pipe;
     auto set_block = [&](const uint32_t k) {
-        const Work wk = decode_work<kCausal>(nwg, xcd + 8 * k, n_qtiles, (int)p.num_heads_q);
+        const Work wk = decode_work<kCausal>(nwg, xcd + 8 * k, n_qtiles, (int)p.num_heads_q, (int)p.head_q_per_group);
         const int hkv = wk.hq / (int)p.head_q_per_group;
         qb = (const char *)p.q_ptr + 2 * ((int64_t)wk.b * p.q_batch_stride + (int64_t)wk.hq * p.q_head_stride);
         kb = (const char *)p.k_ptr + 2 * ((int64_t)wk.b * p.k_batch_stride + (int64_t)hkv * p.k_head_stride);

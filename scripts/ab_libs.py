@@ -52,10 +52,15 @@ dcode = 0 if dt == torch.float16 else 1
 def run(i, n):
     libs[i].fa_debug_set_knobs(variants[i], -1, -1, -1, -1)
     for _ in range(n):
-        assert libs[i].fa_fwd_gfx950(ctypes.byref(ps[i]), dcode, int(cfg["causal"]), ctypes.c_void_p(stream)) == 0
+        if cfg.get("W"):  # local-window configs: fa_fwd_gfx950_window
+            rc = libs[i].fa_fwd_gfx950_window(ctypes.byref(ps[i]), dcode, int(cfg["causal"]),
+                                              ctypes.c_int64(cfg["W"] - 1), ctypes.c_void_p(stream))
+        else:
+            rc = libs[i].fa_fwd_gfx950(ctypes.byref(ps[i]), dcode, int(cfg["causal"]), ctypes.c_void_p(stream))
+        assert rc == 0
 
 
-flops = 4.0 * cfg["B"] * cfg["Hq"] * cfg["Sq"] * cfg["Sk"] * cfg["D"] * (0.5 if cfg["causal"] else 1.0)
+flops = bench.flops(cfg)
 iters = int(os.environ.get("AB_ITERS", "30"))
 for i in range(len(libs)):
     run(i, 10)
