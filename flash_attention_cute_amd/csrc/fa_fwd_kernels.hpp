@@ -810,6 +810,10 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #endif
     constexpr int kQPhase = FA_QPH;  // phase of the tile that issues them
     constexpr int NQP = T / 1024;  // Q pieces per wave (its 64 rows): 16 / 8
+    // a wave's block B starts kRowB rows after its block A (rows interleaved over the waves); the
+    // wave's rows span kRowSpan rows from mw
+    constexpr int kRowB = kBlockM / 2, kRowSpan = kRowB + 32;
+    static_assert(kBlockM == 256, "4 waves x 2 blocks of 32 rows");
     // LDS: K slots 0,1 | V slots 0,1 (64 KiB at D = 128), so every fragment read is a per-lane base
     // plus a 16-bit immediate offset; then (kQL) the Q image, T bytes per wave.
     constexpr int KV0 = 0;
@@ -880,7 +884,10 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         vb = (const char *)p.v_ptr + 2 * (vrow0 + (int64_t)hkv * p.v_head_stride);
         ob = (char *)p.o_ptr + 2 * (orow0 + (int64_t)hq * p.o_head_stride);
         m0 = wk.qtile * kBlockM;
-        mw = m0 + wave * 64;  // block A: rows mw..mw+31, block B: rows mw+32..mw+63
+        // rows interleaved over the waves: block A = rows mw..mw+31 (the workgroup's first half),
+        // block B = rows mw+kRowB.. (its second half), so the last causal diagonal tiles hold no
+        // score of any wave's block A (A-dead tiles, below)
+        mw = m0 + wave * 32;
         n_end = n_blocks;
         if (kCausal) {
             const int x = diag + min(m0 + kBlockM, Sq);
@@ -907,14 +914,14 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     set_block(decode_work<kCausal>(nwg, xcd + 8 * kblk, n_qtiles, (int)p.num_heads_q, (int)p.head_q_per_group));
 
     // ---- Q: this wave's 64 rows, B-operand fragments straight from HBM into AGPRs ----------
-    // lane (h, r) of block X holds Q[mw + 32X + r][16*ks + 8*h + 0..7]; rows >= Sq read as 0.
+    // lane (h, r) of block X holds Q[mw + kRowB*X + r][16*ks + 8*h + 0..7]; rows >= Sq read as 0.
     // Asynchronous: retired by the vmcnt wait ahead of the block's first barrier.
     auto load_q = [&]() __attribute__((always_inline)) {
         const int qs = (int)p.q_seqlen_stride;
-        const rsrc_t qr = make_rsrc(qb + 2 * (int64_t)mw * qs, slab_bytes(min(Sq - mw, 64), qs, D));
+        const rsrc_t qr = make_rsrc(qb + 2 * (int64_t)mw * qs, slab_bytes(min(Sq - mw, kRowSpan), qs, D));
         auto qoff = [&](const int X, const int ks) {
             const bool ok = kExactD || 16 * ks + 8 * h < D;  // columns past D read as 0
-            return ok ? (32 * X + r) * qs * 2 + 32 * ks + 16 * h : 0x7ffffff0;
+            return ok ? (kRowB * X + r) * qs * 2 + 32 * ks + 16 * h : 0x7ffffff0;
         };
         if constexpr (kFold) {
             u32x4 qv[2 * KS];
@@ -938,7 +945,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     const bool rope_q = kExactD && xa.cos != nullptr;
     auto load_q_rope = [&]() __attribute__((always_inline)) {
         const int qs = (int)p.q_seqlen_stride, cs = (int)xa.seq_stride;
-        const int rows = min(Sq - mw, 64);
+        const int rows = min(Sq - mw, kRowSpan);
         const rsrc_t qr = make_rsrc(qb + 2 * (int64_t)mw * qs, slab_bytes(rows, qs, D));
         const rsrc_t cr = make_rsrc(cosb + 2 * (int64_t)mw * cs, slab_bytes(rows, cs, D));
         const rsrc_t sr = make_rsrc(sinb + 2 * (int64_t)mw * cs, slab_bytes(rows, cs, D));
@@ -947,9 +954,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             u32x4 qv[KS], cv[KS], sv[KS];
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
-                qv[ks] = __builtin_amdgcn_raw_buffer_load_b128(qr, (32 * X + r) * qs * 2 + 32 * ks + 16 * h, 0, 0);
-                cv[ks] = __builtin_amdgcn_raw_buffer_load_b128(cr, (32 * X + r) * cs * 2 + 32 * ks + 16 * h, 0, 0);
-                sv[ks] = __builtin_amdgcn_raw_buffer_load_b128(sr, (32 * X + r) * cs * 2 + 32 * ks + 16 * h, 0, 0);
+                qv[ks] = __builtin_amdgcn_raw_buffer_load_b128(qr, (kRowB * X + r) * qs * 2 + 32 * ks + 16 * h, 0, 0);
+                cv[ks] = __builtin_amdgcn_raw_buffer_load_b128(cr, (kRowB * X + r) * cs * 2 + 32 * ks + 16 * h, 0, 0);
+                sv[ks] = __builtin_amdgcn_raw_buffer_load_b128(sr, (kRowB * X + r) * cs * 2 + 32 * ks + 16 * h, 0, 0);
             }
             static_for<KS>([&](auto KK) {
                 constexpr int ks = decltype(KK)::value;
@@ -969,7 +976,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     const uint32_t q_lds = lds_u32(lds) + QOFF + wave * T;  // this wave's Q image
     auto q_piece = [&](const rsrc_t &qr, const int n) __attribute__((always_inline)) {
         const int ch = q_ch0 ^ (4 * (n & (RB == 256 ? 3 : 1)));
-        uint32_t voff = q_lane_off + (uint32_t)(n * ROWS_PER_PIECE * qs_ * 2) + 16u * (uint32_t)ch;
+        // image rows 0..31 are block A's rows mw.., rows 32..63 block B's rows mw+kRowB..
+        const int srow = n * ROWS_PER_PIECE + (n >= NQP / 2 ? kRowB - 32 : 0);
+        uint32_t voff = q_lane_off + (uint32_t)(srow * qs_ * 2) + 16u * (uint32_t)ch;
         if (!kExactD && ch * 8 >= D) voff = 0x7ffffff0u;  // columns past D read as 0
         dma_one(qr, q_lds + n * 1024, (int)voff, true);
     };
@@ -982,9 +991,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             sq = cu_q[wk.b + 1] - q0;
             row0 = (int64_t)q0 * qs_;
         }
-        const int mwn = wk.qtile * kBlockM + wave * 64;
+        const int mwn = wk.qtile * kBlockM + wave * 32;
         const char *qbn = (const char *)p.q_ptr + 2 * (row0 + (int64_t)wk.hq * p.q_head_stride);
-        return make_rsrc_u(qbn + 2 * (int64_t)mwn * qs_, slab_bytes(min(sq - mwn, 64), qs_, D));
+        return make_rsrc_u(qbn + 2 * (int64_t)mwn * qs_, slab_bytes(min(sq - mwn, kRowSpan), qs_, D));
     };
     // the next block (decoded once, in this block's prologue) and its Q pieces: qn of qnt issued
     // (kQL == 2: during this block's tiles)
@@ -1198,10 +1207,13 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // (gap 4ks+2: K_{j+1} pieces, then V_j pieces), and with SM2 the second softmax half of the
     // tile of parity pr (32 units: block u&1, score u>>1 of half 1).
     constexpr int G1 = 4 * KS;
-    auto phase1 = [&](const char *K, auto PAR, auto SM2, auto DMA, const rsrc_t &kr, const rsrc_t &vr)
+    // AD (A-dead tiles, causal diagonal): bit 0 = block A has no visible score in this tile (its S
+    // MFMAs are skipped), bit 1 = nor in the previous tile (its late softmax units are skipped)
+    auto phase1 = [&](const char *K, auto PAR, auto SM2, auto DMA, const rsrc_t &kr, const rsrc_t &vr, auto AD)
         __attribute__((always_inline)) {
         constexpr int c = decltype(PAR)::value, pr = c ^ 1;
         constexpr bool do_sm = decltype(SM2)::value, do_dma = decltype(DMA)::value;
+        constexpr bool sdead = decltype(AD)::value & 1, pdead = decltype(AD)::value & 2;
         u32x4 kf[2][2];  // [buffer][key half]
 #pragma unroll
         for (int x = 0; x < 2; ++x) kf[0][x] = *(const u32x4 *)(K + x * 32 * RB + k_addr[0]);
@@ -1210,8 +1222,12 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             constexpr int ks = g >> 2, i = g & 3, cb = ks & 1;
             // one counted wait per k-step (its two K fragments were read a whole k-step ahead)
             if constexpr (ks > 0 && i == 0) __builtin_amdgcn_s_waitcnt(kLgkm0);
-            if constexpr (kFold && ks == 0) mfma_sq_bias<F, QB + 4 * ((i >> 1) * KS + ks)>(S[c][i], kf[cb][i & 1], bias[i >> 1]);
-            else mfma_sq<F, QB + 4 * ((i >> 1) * KS + ks)>(ks == 0, S[c][i], kf[cb][i & 1]);
+            if constexpr (sdead && i < 2) {
+            } else if constexpr (kFold && ks == 0) {
+                mfma_sq_bias<F, QB + 4 * ((i >> 1) * KS + ks)>(S[c][i], kf[cb][i & 1], bias[i >> 1]);
+            } else {
+                mfma_sq<F, QB + 4 * ((i >> 1) * KS + ks)>(ks == 0, S[c][i], kf[cb][i & 1]);
+            }
             // the MFMA alone in its scheduling region: the pre-RA scheduler would otherwise hoist
             // this gap's (independent) VALU above it, into the previous gap
             FA_SCHED_FENCE();
@@ -1233,7 +1249,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             if constexpr (do_sm) {
                 static_for<kNL>([&](auto U) {
                     constexpr int u = decltype(U)::value;
-                    if constexpr ((u * G1) / kNL == g) {
+                    if constexpr ((u * G1) / kNL == g && !(pdead && (u & 1) == 0)) {
                         u_exp(pr, u & 1, Late::hf(u), Late::v(u));
                         if constexpr (u >= 2) u_fin(pr, u & 1, Late::hf(u - 2), Late::v(u - 2));
                     }
@@ -1242,18 +1258,21 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             FA_SCHED_FENCE();
         });
         if constexpr (do_sm) {
-            u_fin(pr, 0, Late::hf(kNL - 2), Late::v(kNL - 2));
+            if constexpr (!pdead) u_fin(pr, 0, Late::hf(kNL - 2), Late::v(kNL - 2));
             u_fin(pr, 1, Late::hf(kNL - 1), Late::v(kNL - 1));
         }
     };
     // the same second softmax half without MFMAs (drain and masked tiles)
-    auto sm2_all = [&](auto PAR) __attribute__((always_inline)) {
+    auto sm2_all = [&](auto PAR, auto AD) __attribute__((always_inline)) {
         constexpr int c = decltype(PAR)::value;
+        constexpr int X0 = (decltype(AD)::value & 2) ? 1 : 0;  // (block A dead in tile c: B only)
         static_for<32 - kV0>([&](auto VV) {  // the late scores
             constexpr int q = kV0 + decltype(VV)::value;
             static_for<2>([&](auto XX) {
-                u_exp(c, decltype(XX)::value, q >> 4, q & 15);
-                u_fin(c, decltype(XX)::value, q >> 4, q & 15);
+                if constexpr (decltype(XX)::value >= X0) {
+                    u_exp(c, decltype(XX)::value, q >> 4, q & 15);
+                    u_fin(c, decltype(XX)::value, q >> 4, q & 15);
+                }
             });
         });
     };
@@ -1297,9 +1316,12 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         }
         return true;
     }(), "phase-2 softmax schedule");
-    auto phase2 = [&](const char *V, auto PPV, auto PSM, auto SM1) __attribute__((always_inline)) {
+    // AD: bit 0 = block A has no visible score in tile cs (its early softmax units are skipped),
+    // bit 1 = nor in tile cp (its P.V MFMAs are skipped: P is 0)
+    auto phase2 = [&](const char *V, auto PPV, auto PSM, auto SM1, auto AD) __attribute__((always_inline)) {
         constexpr int cp = decltype(PPV)::value, cs = decltype(PSM)::value;
         constexpr bool do_sm = decltype(SM1)::value;
+        constexpr bool sdead = decltype(AD)::value & 1, pdead = decltype(AD)::value & 2;
         u32x4 va[2][DTL];
         auto rd = [&](const int kk, const int n, u32x4 *dst) {
             const int rowoff = ((kk >> 1) * 32 + (kk & 1) * 16) * RB + (n & 1) * 8 * RB;
@@ -1316,7 +1338,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             // one counted wait per 16-key step: its V^T fragments were read in the first DTL gaps
             // of the previous step, two per gap
             if constexpr (kk > 0 && i == 0) __builtin_amdgcn_s_waitcnt(kLgkm0);
-            agpr_mfma<F, X * 16 * DTL + 16 * dt>(va[kk & 1][dt], P[cp][4 * X + kk]);
+            if constexpr (!(pdead && X == 0)) agpr_mfma<F, X * 16 * DTL + 16 * dt>(va[kk & 1][dt], P[cp][4 * X + kk]);
             FA_SCHED_FENCE();  // (see phase 1)
             if constexpr (kk + 1 < 4 && i < DTL) {
                 rd(kk + 1, 2 * i, va[(kk + 1) & 1]);
@@ -1332,16 +1354,18 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             if constexpr (do_sm) {
                 static_for<32>([&](auto M) {
                     constexpr int X2 = decltype(M)::value >> 4, m = decltype(M)::value & 15;
-                    if constexpr (Ex::max_gap(X2, m) == g) u_max(cs, X2, m);
+                    if constexpr (Ex::max_gap(X2, m) == g && !(sdead && X2 == 0)) u_max(cs, X2, m);
                 });
                 static_for<4>([&](auto K2) {
                     constexpr int X2 = decltype(K2)::value >> 1, k = decltype(K2)::value & 1;
-                    if constexpr (Ex::dec_gap(X2, k) == g) u_dec(cs, X2, k);
+                    if constexpr (Ex::dec_gap(X2, k) == g && !(sdead && X2 == 0)) u_dec(cs, X2, k);
                 });
                 static_for<NE>([&](auto E) {
                     constexpr int e = decltype(E)::value;
-                    if constexpr (Ex::gap(e) + 1 == g) u_fin(cs, Ex::blk(e), Ex::v(e) >> 4, Ex::v(e) & 15);
-                    if constexpr (Ex::gap(e) == g) u_exp(cs, Ex::blk(e), Ex::v(e) >> 4, Ex::v(e) & 15);
+                    if constexpr (!(sdead && Ex::blk(e) == 0)) {
+                        if constexpr (Ex::gap(e) + 1 == g) u_fin(cs, Ex::blk(e), Ex::v(e) >> 4, Ex::v(e) & 15);
+                        if constexpr (Ex::gap(e) == g) u_exp(cs, Ex::blk(e), Ex::v(e) >> 4, Ex::v(e) & 15);
+                    }
                 });
             }
             FA_SCHED_FENCE();
@@ -1349,7 +1373,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         if constexpr (do_sm) {
             static_for<NE>([&](auto E) {
                 constexpr int e = decltype(E)::value;
-                if constexpr (Ex::gap(e) == G2 - 1) u_fin(cs, Ex::blk(e), Ex::v(e) >> 4, Ex::v(e) & 15);
+                if constexpr (Ex::gap(e) == G2 - 1 && !(sdead && Ex::blk(e) == 0))
+                    u_fin(cs, Ex::blk(e), Ex::v(e) >> 4, Ex::v(e) & 15);
             });
         }
     };
@@ -1451,8 +1476,17 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             }
         }
     };
+    // MASKED: 0 = no masked score, 1 = masked (diagonal / tail / window), 2 = masked and block A
+    // dead in tile j (no row of any wave's block A sees a key of it), 3 = A dead in tiles j and j-1
     auto iter = [&](const int j, auto PAR, auto MASKED) __attribute__((always_inline)) {
         constexpr int c = decltype(PAR)::value, pr = c ^ 1;
+        constexpr int mk = decltype(MASKED)::value;
+        using AD = IC<mk == 2 ? 1 : mk == 3 ? 3 : 0>;
+        if constexpr (mk >= 2) {  // block A takes no decision and adds no row sum in tile j
+            st[0].rmask = 0;
+            st[0].resc = false;
+            st[0].t = 0.f;
+        }
         FA_STAMP(sa);
         const rsrc_t kr = make_rsrc(kp, tile_bytes((j + 1) * kBlockN, full_k, ks_));
         const rsrc_t vr = make_rsrc(vp, tile_bytes(j * kBlockN, full_v, vs_));
@@ -1460,23 +1494,25 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         vp += step_v;
         // FA_EXP_*: timing experiments of the stamps build only (results are garbage)
 #if defined(FA_EXP_NOSM)
-        phase1(lds + KV0 + c * T, PAR, IC<0>{}, IC<1>{}, kr, vr);
+        phase1(lds + KV0 + c * T, PAR, IC<0>{}, IC<1>{}, kr, vr, AD{});
 #elif defined(FA_EXP_NODMA)
-        phase1(lds + KV0 + c * T, PAR, IC<1>{}, IC<0>{}, kr, vr);
+        phase1(lds + KV0 + c * T, PAR, IC<1>{}, IC<0>{}, kr, vr, AD{});
 #else
-        phase1(lds + KV0 + c * T, PAR, IC<1>{}, IC<1>{}, kr, vr);
+        phase1(lds + KV0 + c * T, PAR, IC<1>{}, IC<1>{}, kr, vr, AD{});
 #endif
-        if constexpr (decltype(MASKED)::value) {  // diagonal / tail tile: mask S before phase 2
-            s_ready(S[c][0], S[c][1]);
+        if constexpr (mk != 0) {  // diagonal / tail tile: mask S before phase 2
+            if constexpr (mk == 1) {
+                s_ready(S[c][0], S[c][1]);
+                mask(S[c][0], S[c][1], mw + r, j * kBlockN);
+            }
             s_ready(S[c][2], S[c][3]);
-            mask(S[c][0], S[c][1], mw + r, j * kBlockN);
-            mask(S[c][2], S[c][3], mw + 32 + r, j * kBlockN);
+            mask(S[c][2], S[c][3], mw + kRowB + r, j * kBlockN);
         }
         FA_STAMP(sb);
 #if defined(FA_EXP_NOSM)
-        phase2(lds + KV0 + (2 + pr) * T, IC<pr>{}, PAR, IC<0>{});
+        phase2(lds + KV0 + (2 + pr) * T, IC<pr>{}, PAR, IC<0>{}, AD{});
 #else
-        phase2(lds + KV0 + (2 + pr) * T, IC<pr>{}, PAR, IC<1>{});
+        phase2(lds + KV0 + (2 + pr) * T, IC<pr>{}, PAR, IC<1>{}, AD{});
 #endif
         rescale(j == j_lo);
         FA_STAMP(sc_);
@@ -1513,14 +1549,33 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         iter(t, IC<0>{}, IC<0>{});
         if (t + 1 < n_unm) iter(t + 1, IC<1>{}, IC<0>{});
     }
+    // causal: the tiles from jA on hold no visible score of any wave's block A (its rows are the
+    // workgroup's first half): they run B only (MASKED 2, then 3)
+    int jA = n_loop;
+    if (kCausal) {
+        const int x = min(Sk - 1, m0 + kRowSpan - 1 + diag);  // the last visible key of block A
+        jA = x < 0 ? 0 : x / kBlockN + 1;
+    }
     {
         j = max(j, n_unm);
-        if (((j - j_lo) & 1) && j < n_loop) iter(j++, IC<1>{}, IC<1>{});
-        for (; j < n_loop; j += 2) {
+        const int j0 = j, jm = min(max(jA, j), n_loop);
+        if (((j - j_lo) & 1) && j < jm) iter(j++, IC<1>{}, IC<1>{});
+        for (; j < jm; j += 2) {
             iter(j, IC<0>{}, IC<1>{});
-            if (j + 1 < n_loop) iter(j + 1, IC<1>{}, IC<1>{});
+            if (j + 1 < jm) iter(j + 1, IC<1>{}, IC<1>{});
+        }
+        j = max(j0, jm);  // (the pair loop may step past jm)
+        if constexpr (kCausal) {
+            if (j < n_loop) {
+                if ((j - j_lo) & 1) iter(j, IC<1>{}, IC<2>{}); else iter(j, IC<0>{}, IC<2>{});
+                ++j;
+            }
+            for (; j < n_loop; ++j) {
+                if ((j - j_lo) & 1) iter(j, IC<1>{}, IC<3>{}); else iter(j, IC<0>{}, IC<3>{});
+            }
         }
     }
+    const bool last_dead = kCausal && n_loop > max(jA, j_lo);  // the last pipelined tile is A-dead
     FA_STAMP(s_loop_end);
     // ---- debug variant: every tile masked, not pipelined -----------------------------------
     if (n_loop < n_end) {
@@ -1537,15 +1592,15 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         const char *K = lds + KV0 + sl * T;
         const char *V = lds + KV0 + (2 + sl) * T;
         const int key0 = j * kBlockN;
-        phase1(K, IC<0>{}, IC<0>{}, IC<0>{}, k_rsrc(j), k_rsrc(j));
+        phase1(K, IC<0>{}, IC<0>{}, IC<0>{}, k_rsrc(j), k_rsrc(j), IC<0>{});
         s_ready(S[0][0], S[0][1]);
         s_ready(S[0][2], S[0][3]);
         mask(S[0][0], S[0][1], mw + r, key0);
-        mask(S[0][2], S[0][3], mw + 32 + r, key0);
+        mask(S[0][2], S[0][3], mw + kRowB + r, key0);
         sm1_all(IC<0>{});
         rescale(j == j_lo);
-        sm2_all(IC<0>{});
-        phase2(V, IC<0>{}, IC<0>{}, IC<0>{});
+        sm2_all(IC<0>{}, IC<0>{});
+        phase2(V, IC<0>{}, IC<0>{}, IC<0>{}, IC<0>{});
         dma_wait();
         __syncthreads();
     }
@@ -1575,20 +1630,26 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         if (q_in_agpr) q_from_lds();
     }
     // drain the last pipelined tile: softmax half 2 and P.V
-    auto drain = [&](auto PAR) __attribute__((always_inline)) {
+    auto drain = [&](auto PAR, auto AD) __attribute__((always_inline)) {
         constexpr int c = decltype(PAR)::value;
-        sm2_all(PAR);
-        phase2(lds + KV0 + (2 + c) * T, PAR, PAR, IC<0>{});
+        sm2_all(PAR, AD);
+        phase2(lds + KV0 + (2 + c) * T, PAR, PAR, IC<0>{}, AD);
     };
     if (n_loop > jlo_c) {  // (set_block above moved j_lo to the next block)
-        if ((n_loop - 1 - jlo_c) & 1) drain(IC<1>{}); else drain(IC<0>{});
+        if (kCausal && last_dead) {
+            if constexpr (kCausal) {
+                if ((n_loop - 1 - jlo_c) & 1) drain(IC<1>{}, IC<2>{}); else drain(IC<0>{}, IC<2>{});
+            }
+        } else {
+            if ((n_loop - 1 - jlo_c) & 1) drain(IC<1>{}, IC<0>{}); else drain(IC<0>{}, IC<0>{});
+        }
     }
     FA_STAMP(s_pipe_end);
 
     // ---- epilogue ---------------------------------------------------------------------------
     mfma_drain();  // last asm MFMA -> AGPR reads
     const int os_ = (int)p.o_seqlen_stride;
-    const rsrc_t orr = make_rsrc(ob_c + 2 * (int64_t)mw_c * os_, slab_bytes(min(sq_c - mw_c, 64), os_, D));
+    const rsrc_t orr = make_rsrc(ob_c + 2 * (int64_t)mw_c * os_, slab_bytes(min(sq_c - mw_c, kRowSpan), os_, D));
     auto store_block = [&](const int row, auto OBASE, const float l_tot) {
         constexpr int ob0 = decltype(OBASE)::value;
         f32x16 o[DTL];
@@ -1623,7 +1684,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     const float l0 = pair_sum(st[0].l);
     const float l1 = pair_sum(st[1].l);
     store_block(r, IC<0>{}, l0);
-    store_block(r + 32, IC<16 * DTL>{}, l1);
+    store_block(r + kRowB, IC<16 * DTL>{}, l1);
 #ifdef FA_STAMPS
     {
         __builtin_amdgcn_s_waitcnt(0);
