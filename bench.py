@@ -20,8 +20,9 @@ reference models/rope_attn_fwd.py:66-120 with this repo's fused RoPE) -- value i
 bare op and unpatched HF (SDPA) timed beside it in the same run.
 
 Rank 0 prints ONE JSON line. Besides the contract fields it carries
-  roofline     : the kernel's achieved TFLOP/s (algorithmic FLOPs / mean HIP-event duration of
-                 the launches in the timed region) against the dense fp16 MFMA peak; ``traffic`` is
+  roofline     : the kernel's achieved TFLOP/s (algorithmic FLOPs / the HIP-event time of the
+                 timed region's back-to-back launches, per launch) against the dense fp16 MFMA
+                 peak; ``traffic`` is
                  the HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/), or null;
   cpu_baseline : torch SDPA fp32 on the host cores (the reference op's CPU path, BASELINE.md's CPU
                  baseline) on the same workload; ``port`` = oracle/fa_oracle.c on a bounded sample.
@@ -365,16 +366,21 @@ def main() -> None:
         extra["layer"] = layer_info
 
     def timed(fn, n):
-        """n calls of fn between synchronisations: (wall s, mean HIP-event ms per call)."""
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+        """n back-to-back calls of fn between synchronisations: (wall s, HIP-event ms per call).
+
+        One event pair brackets the n launches on the current stream (the stream the kernel runs
+        on). An event pair around EVERY launch, as round 1 / 2 had it, puts ≈6-10 µs between
+        consecutive kernels on ROCm (rocprof kernel trace: 0 µs between back-to-back launches, ≈10 µs
+        with the per-launch records), which is measurement overhead, not the op's."""
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for i in range(n):
-            ev[i][0].record()
+        a.record()
+        for _ in range(n):
             fn()
-            ev[i][1].record()
+        b.record()
         torch.cuda.synchronize()
-        return time.perf_counter() - t0, sum(a.elapsed_time(b) for a, b in ev) / n
+        return time.perf_counter() - t0, a.elapsed_time(b) / n
 
     main_step = layer_step if layer else step
     # Device warm-up: the MI355X ramps its clock over the first ~second of sustained load, so a
