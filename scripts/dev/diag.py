@@ -2,7 +2,7 @@
 import sys
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 import torch  # noqa: E402
 
 from flash_attention_cute_amd import flash_attn_func  # noqa: E402

@@ -1,4 +1,5 @@
 set -o pipefail
+# GPU box only: it copies ab/<lib>.so over the box copy of the product library between passes (gpurun snapshots are discarded).
 R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/icache; mkdir -p $OUT
 export TMPDIR=/tmp; cd /tmp
