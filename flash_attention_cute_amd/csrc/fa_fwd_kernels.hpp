@@ -13,7 +13,8 @@
 //
 // Two prefill kernels (DESIGN.md section 4 has the numbers):
 //   * fa_fwd_w4 (default): persistent grid, one workgroup per CU walking Q blocks of 256 query rows
-//     of one (batch, q-head); 4 wave64s, one per SIMD, each owning 64 rows (two 32-row blocks)
+//     of one (batch, q-head); 4 wave64s, one per SIMD, each owning 64 rows (two 32-row blocks,
+//     one in each half of the Q block, so the last causal diagonal tiles run one block only)
 //     with the whole 512-register file: O^T and the Q fragments in literal AGPRs (fa_agpr_asm.inc),
 //     K/V tiles of 64 keys by LDS-DMA into 2-slot rings, a two-phase software pipeline per tile
 //     (S = K.Q^T beside the previous tile's softmax tail; O += P.V beside this tile's max, rescale
