@@ -11,9 +11,12 @@ inputs and stores inputs + outputs as fixtures:
   golden_c1.npz      BASELINE config 1: fp32 B1 H2 S128 D64, no mask (seed 0, q, k, v order)
   golden_small.npz   fp32 / fp16 / bf16 cases, causal and not, Sq == Sk (where the reference's
                      top-left CPU causal equals the kernel's bottom-right causal)
+  golden_multi.npz   fp16 / bf16 cases at multi-block sizes (see MULTI_SPEC): several Q blocks and
+                     >= 10 KV tiles, Sq != Sk, Sq == 1, D in {40, 72, 100}, a strided input
   golden_meta.json   the op schema and the reference's error on a GQA call on CPU
 
 No bytecode is written into /root/reference. Re-run with:  python tests/golden/make_golden.py
+(``--multi`` regenerates only golden_multi.npz).
 """
 from __future__ import annotations
 
@@ -49,8 +52,58 @@ def to_np(t: torch.Tensor) -> np.ndarray:
     return t.numpy()
 
 
+# Multi-block cases (golden_multi.npz): sizes the gfx950 kernel actually tiles -- several 256-row Q
+# blocks, >= 10 64-key KV tiles, ragged tails, Sq != Sk, Sq == 1 (the GPU's q-head pack path),
+# head dims off the two native tiles (40, 72) and one the GPU wrapper pads (100), and a strided
+# (transposed-view) input. The reference's CPU path is top-left causal, so causal cases keep
+# Sq == Sk (where top-left == bottom-right); Sq != Sk and Sq == 1 cases are non-causal (the
+# reference forces non-causal at Sq == 1 on the GPU anyway, csrc/flash_attention_api.cpp:81).
+#  (name, dtype, B, H, Sq, Sk, D, causal, layout)   layout "bhsd" contiguous | "bshd" = HF view
+MULTI_SPEC = [
+    ("f16", torch.float16, 1, 1, 640, 640, 64, False, "bhsd"),
+    ("bf16", torch.bfloat16, 1, 1, 600, 600, 128, True, "bhsd"),
+    ("f16", torch.float16, 1, 1, 600, 600, 64, True, "bhsd"),
+    ("f16", torch.float16, 1, 1, 130, 900, 64, False, "bhsd"),
+    ("bf16", torch.bfloat16, 1, 1, 700, 130, 64, False, "bhsd"),
+    ("f16", torch.float16, 1, 2, 1, 520, 64, False, "bhsd"),
+    ("bf16", torch.bfloat16, 2, 1, 1, 300, 128, False, "bhsd"),
+    ("f16", torch.float16, 1, 1, 300, 300, 40, True, "bhsd"),
+    ("bf16", torch.bfloat16, 1, 1, 333, 333, 72, False, "bhsd"),
+    ("f16", torch.float16, 1, 1, 260, 260, 100, True, "bhsd"),
+    ("bf16", torch.bfloat16, 1, 2, 280, 280, 64, True, "bshd"),
+]
+
+
+def make_multi(ref) -> int:
+    cases = {}
+    for i, (name, dt, b, h, sq, sk, d, causal, layout) in enumerate(MULTI_SPEC):
+        torch.manual_seed(1000 + i)
+        if layout == "bshd":  # HF projection layout: [B, S, H, D] storage, [B, H, S, D] views
+            q, k, v = (torch.randn(b, s, h, d).to(dt).transpose(1, 2) for s in (sq, sk, sk))
+        else:
+            q, k, v = (torch.randn(b, h, s, d).to(dt) for s in (sq, sk, sk))
+        o = ref.flash_attn_func(q, k, v, causal=causal)  # default scale D ** -0.5 (reference :52)
+        key = f"case{i}"
+        # store the [B, H, S, D] values contiguously; the test rebuilds the strided view from layout
+        cases[f"{key}_q"], cases[f"{key}_k"], cases[f"{key}_v"], cases[f"{key}_o"] = (
+            to_np(t.contiguous()) for t in (q, k, v, o))
+        cases[f"{key}_meta"] = np.array([b, h, sq, sk, d, int(causal)], dtype=np.int64)
+        cases[f"{key}_dtype"] = np.array(name)
+        cases[f"{key}_layout"] = np.array(layout)
+        cases[f"{key}_scale"] = np.float64(d ** -0.5)
+    np.savez_compressed(OUT / "golden_multi.npz", **cases)
+    return len(MULTI_SPEC)
+
+
 def main() -> None:
     ref = import_reference_op()
+    if "--multi" in sys.argv:  # regenerate only golden_multi.npz (+ its count in golden_meta.json)
+        warnings.simplefilter("ignore")
+        meta = json.loads((OUT / "golden_meta.json").read_text())
+        meta["n_multi_cases"] = make_multi(ref)
+        (OUT / "golden_meta.json").write_text(json.dumps(meta, indent=1) + "\n")
+        print(json.dumps(meta, indent=1))
+        return
     warnings.simplefilter("ignore")
     schema = str(torch.ops.flash_attention.forward.default._schema)
 
@@ -89,7 +142,7 @@ def main() -> None:
         gqa_err = None
     except RuntimeError as e:
         gqa_err = str(e).splitlines()[0]
-    meta = {"schema": schema, "cpu_gqa_error": gqa_err, "n_small_cases": len(spec),
+    meta = {"schema": schema, "cpu_gqa_error": gqa_err, "n_small_cases": len(spec), "n_multi_cases": make_multi(ref),
             "generator": "reference flash_attention/flash_attention.py CPU path, torch " + torch.__version__}
     (OUT / "golden_meta.json").write_text(json.dumps(meta, indent=1) + "\n")
     print(json.dumps(meta, indent=1))

@@ -65,6 +65,57 @@ def test_reference_golden_vectors_on_gpu(op, device):
     assert ran == 5
 
 
+def test_reference_golden_multi_block_vectors_on_gpu(op, device):
+    """The multi-block fixtures the REFERENCE's op produced (tests/golden/golden_multi.npz: several
+    256-row Q blocks, >= 10 KV tiles, Sq != Sk, Sq == 1 -> the q-head pack / decode kernel, D 40 / 72,
+    D 100 through the pad wrapper, an HF [B, S, H, D] strided view) through the HIP op."""
+    from flash_attention_cute_amd import _debug
+
+    g = np.load(GOLD / "golden_multi.npz")
+    n = json.loads((GOLD / "golden_meta.json").read_text())["n_multi_cases"]
+    paths = []
+    for i in range(n):
+        dtype = str(g[f"case{i}_dtype"])
+        b, h, sq, sk, d, causal = (int(x) for x in g[f"case{i}_meta"])
+        q, k, v, ref = (_gold_tensor(g[f"case{i}_{n_}"], dtype) for n_ in "qkvo")
+        if str(g[f"case{i}_layout"]) == "bshd":  # rebuild the HF view: [B, S, H, D] storage
+            q, k, v = (t.transpose(1, 2).contiguous().to(device).transpose(1, 2) for t in (q, k, v))
+            assert q.stride(2) == h * d
+        else:
+            q, k, v = q.to(device), k.to(device), v.to(device)
+        out = op(q, k, v, causal=bool(causal))
+        paths.append(_debug.last_path())
+        out = out.float().cpu()
+        tol = {"f16": 2e-3, "bf16": 1.6e-2}[dtype]
+        err = (out - ref.float()).abs()
+        assert (err <= tol + tol * ref.float().abs()).all(), (i, err.max().item())
+        assert err.mean().item() < tol / 8, (i, err.mean().item())
+    assert n == 11
+    # Sq == 1 cases ran the decode (pack) kernel, every other case the persistent prefill kernel
+    metas = [int(g[f"case{i}_meta"][2]) for i in range(n)]
+    assert all(p.startswith("decode") for p, s in zip(paths, metas) if s == 1), paths
+    assert all(p == "w4" for p, s in zip(paths, metas) if s > 1), paths
+
+
+@pytest.mark.parametrize("causal", [False, True])
+def test_reference_module_path_pybind_call_matches_flash_attn_func(op, device, causal):
+    """Code written against the reference's submodule: ``flash_attention.flash_attention
+    .flash_attention_cuda.flash_attention_fwd(q, k, v, scale, causal)`` (reference
+    flash_attention/flash_attention.py:4, :35) is the gfx950 kernel, bit for bit ``flash_attn_func``."""
+    import flash_attention.flash_attention as ref_path
+
+    torch.manual_seed(3)
+    q = torch.randn(2, 8, 333, 128, device=device, dtype=torch.float16)
+    k = torch.randn(2, 2, 333, 128, device=device, dtype=torch.float16)
+    v = torch.randn(2, 2, 333, 128, device=device, dtype=torch.float16)
+    a = ref_path.flash_attention_cuda.flash_attention_fwd(q, k, v, 128 ** -0.5, causal)
+    b = ref_path.flash_attn_func(q, k, v, causal=causal)
+    c = op(q, k, v, causal=causal)
+    assert torch.equal(a, b) and torch.equal(a, c)
+    d = ref_path.flash_attention_forward(q, k, v, 128 ** -0.5, causal)  # the op object itself
+    assert torch.equal(a, d)
+
+
 FULL = [  # (name, B, Hq, Hkv, S, dtype, causal)
     ("C2", 4, 32, 32, 4096, torch.float16, False),
     ("C3", 4, 32, 32, 8192, torch.bfloat16, True),

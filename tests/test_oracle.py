@@ -51,6 +51,40 @@ def test_golden_small_cases(i):
     assert np.abs(out - o).mean() < atol / 8
 
 
+def load_multi_case(g, i):
+    """(q, k, v, o) float64 [B, H, S, D], dtype name, scale, causal, layout of golden_multi case i."""
+    dtype = str(g[f"case{i}_dtype"])
+    b, h, sq, sk, d, causal = (int(x) for x in g[f"case{i}_meta"])
+    q, k, v, o = (as_f64(g[f"case{i}_{n}"], dtype) for n in "qkvo")
+    assert q.shape == (b, h, sq, d) and k.shape == (b, h, sk, d) and o.shape == q.shape
+    return q, k, v, o, dtype, float(g[f"case{i}_scale"]), bool(causal), str(g[f"case{i}_layout"])
+
+
+@pytest.mark.parametrize("i", range(json.loads((GOLD / "golden_meta.json").read_text())["n_multi_cases"]))
+def test_golden_multi_block_cases(i):
+    """Multi-block reference-generated cases (several Q blocks, >= 10 KV tiles, Sq != Sk, Sq == 1,
+    D in {40, 72, 100}, strided input): the restatement agrees with the reference's op."""
+    g = np.load(GOLD / "golden_multi.npz")
+    q, k, v, o, dtype, scale, causal, _ = load_multi_case(g, i)
+    out = O.flash_attention_fwd(q, k, v, scale, causal, dtype)
+    atol = {"f16": 2e-3, "bf16": 1.6e-2}[dtype]
+    np.testing.assert_allclose(out, o, atol=atol, rtol=atol)
+    assert np.abs(out - o).mean() < atol / 8
+
+
+def test_golden_multi_covers_the_kernel_shapes():
+    g = np.load(GOLD / "golden_multi.npz")
+    n = json.loads((GOLD / "golden_meta.json").read_text())["n_multi_cases"]
+    metas = [tuple(int(x) for x in g[f"case{i}_meta"]) for i in range(n)]
+    assert any(sq == sk and sq > 512 and c for _, _, sq, sk, _, c in metas)  # causal, >= 3 Q blocks
+    assert any(sq == sk and sq > 512 and not c for _, _, sq, sk, _, c in metas)
+    assert any(sk >= 640 for _, _, _, sk, _, _ in metas)  # >= 10 KV tiles
+    assert any(1 < sq < sk for _, _, sq, sk, _, _ in metas) and any(sq > sk for _, _, sq, sk, _, _ in metas)
+    assert any(sq == 1 for _, _, sq, _, _, _ in metas)
+    assert {40, 72, 100} <= {d for *_, d, _ in metas}
+    assert "bshd" in {str(g[f"case{i}_layout"]) for i in range(n)}
+
+
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16], ids=["f16", "bf16"])
 @pytest.mark.parametrize("causal", [False, True])
 @pytest.mark.parametrize("shape", [(1, 4, 2, 100, 130, 64), (2, 4, 1, 1, 77, 128), (1, 2, 2, 129, 65, 40),
