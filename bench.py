@@ -51,9 +51,10 @@ CONFIGS = {
                D=128, dtype="bf16", causal=True),
     "c4": dict(workload="C4 GQA fp16 B4 Hq32 Hkv8 S4096 D128 causal", B=4, Hq=32, Hkv=8, Sq=4096,
                Sk=4096, D=128, dtype="fp16", causal=True),
-    # C5: Llama-3-8B attention (Hq32 Hkv8 D128), bf16 causal prefill S4096; global batch 8 sharded
-    # over (batch, kv-head) units -- one batch row per GPU at N=8 (flash_attention_cute_amd/shard.py)
-    "c5": dict(workload="C5 Llama-3-8B attn bf16 causal B1(per GPU) Hq32 Hkv8 S4096 D128", B=1, Hq=32, Hkv=8,
+    # C5: Llama-3-8B attention (Hq32 Hkv8 D128), bf16 causal prefill S4096; by default global batch 8
+    # sharded over (batch, kv-head) units -- one batch row per GPU at N=8 (flash_attention_cute_amd/
+    # shard.py, strong scaling); --weak: a B1 replica per GPU
+    "c5": dict(workload="C5 Llama-3-8B attn bf16 causal Hq32 Hkv8 S4096 D128, B1 per replica", B=1, Hq=32, Hkv=8,
                Sq=4096, Sk=4096, D=128, dtype="bf16", causal=True),
     # the patched HF attention layer around the op at C5's dims (prefill of S tokens, B per GPU)
     "c5_layer": dict(workload="C5 layer: patched Llama-3-8B LlamaAttention.forward bf16 causal B1(per GPU) S4096 "
@@ -69,6 +70,12 @@ CONFIGS = {
     # window of 4096 on Llama-3-8B attention dims, 32k-token prefill); flash_attn_window_func
     "window": dict(workload="sliding window GQA bf16 B1 Hq32 Hkv8 S32768 W4096 D128 causal", B=1, Hq=32, Hkv=8,
                    Sq=32768, Sk=32768, D=128, dtype="bf16", causal=True, W=4096),
+    # a decode step of a left-padded batch (HF generate): the KV cache [B, Hkv, 4096, D] read in
+    # place, sequence b's real keys the last lens[b] positions (mixed lengths 1024 .. 4000);
+    # flash_attn_padded_func -> q-head pack + split-KV decode kernel on each sequence's key range
+    "decode_padded": dict(workload="padded decode GQA bf16 B32 Hq32 Hkv8 Sq1 Sk<=4096 (lens 1024..4000, left "
+                                   "padding) D128", B=32, Hq=32, Hkv=8, Sq=1, Sk=4096, D=128, dtype="bf16",
+                          causal=True, lens=[1024 + 96 * i for i in range(32)]),
 }
 
 
@@ -82,6 +89,8 @@ def metric_of(key: str, c) -> str:
 
 
 def flops(c) -> float:
+    if c.get("lens"):  # padded batch: each row's real keys
+        return 4.0 * c["Hq"] * c["Sq"] * c["D"] * sum(c["lens"][:c["B"]])
     if c.get("W"):  # visible (query, key) pairs under the causal window (Sq == Sk >= W)
         w, s_ = c["W"], c["Sq"]
         return 4.0 * c["B"] * c["Hq"] * c["D"] * (w * (w + 1) / 2 + (s_ - w) * w)
@@ -90,7 +99,17 @@ def flops(c) -> float:
 
 
 def algo_bytes(c) -> int:
+    if c.get("lens"):  # padded batch: q / o of every row, K / V of the real keys only
+        return (2 * c["B"] * c["Hq"] * c["Sq"] * c["D"] + 2 * c["Hkv"] * c["D"] * sum(c["lens"][:c["B"]])) * 2
     return (2 * c["B"] * c["Hq"] * c["Sq"] * c["D"] + 2 * c["B"] * c["Hkv"] * c["Sk"] * c["D"]) * 2
+
+
+def lib_sha16() -> str:
+    """First 16 hex digits of the sha256 of the C-ABI library in the tree (the one the op loads)."""
+    import hashlib
+
+    p = ROOT / "flash_attention_cute_amd" / "lib" / "libfa_gfx950.so"
+    return hashlib.sha256(p.read_bytes()).hexdigest()[:16] if p.exists() else "missing"
 
 
 def cpu_model() -> str:
@@ -114,6 +133,31 @@ def cpu_baseline(q, k, v, c, target_s: float) -> dict:
     torch.set_num_threads(cores)
     f_all = flops(c)
     nb = c["B"] if f_all <= 20 * 1.5e12 else 1  # SDPA fp32 runs ~1.5 TFLOP/s on 16 EPYC cores
+    if c.get("lens"):  # padded decode: per sequence on its real keys
+        try:
+            qf, kf, vf = (t.float().cpu() for t in (q, k, v))
+            sk = c["Sk"]
+
+            def run_all():
+                for b, n in enumerate(c["lens"][:c["B"]]):
+                    torch.nn.functional.scaled_dot_product_attention(qf[b:b + 1], kf[b:b + 1, :, sk - n:],
+                                                                     vf[b:b + 1, :, sk - n:], enable_gqa=True)
+            run_all()
+            nrep = 5
+            t0 = time.perf_counter()
+            for _ in range(nrep):
+                run_all()
+            t_sdpa = (time.perf_counter() - t0) / nrep
+            gbs = algo_bytes(c) / t_sdpa / 1e9
+            return {"value": round(gbs, 3), "unit": "GB/s", "cores": torch.get_num_threads(), "kind": "reference",
+                    "tflops": round(f_all / t_sdpa / 1e12, 6),
+                    "sample": f"the whole workload ({c['workload']}, {t_sdpa * 1e3:.2f} ms per step, mean of {nrep} "
+                              "after 1 warm-up): torch SDPA fp32 per sequence on its real keys, the reference op's "
+                              "CPU path (flash_attention/flash_attention.py:6-15); bf16 algorithmic bytes",
+                    "cpu_model": cpu_model()}
+        except Exception as e:  # noqa: BLE001
+            return {"value": None, "unit": "GB/s", "cores": cores, "kind": "reference", "error": repr(e),
+                    "cpu_model": cpu_model()}
     try:
         qf, kf, vf = (t[:nb].float().cpu() for t in (q, k, v))
         causal = c["causal"] and c["Sq"] > 1
@@ -201,13 +245,20 @@ def cpu_port(q, k, v, c, target_s: float, cores: int) -> dict:
 
 
 def load_traffic(config_key: str):
+    """(HBM bytes per launch, provenance) from profiles/pmc_<config>.json -- only when that PMC pass
+    profiled THIS library (its ``lib_sha16`` equals the loaded library's); otherwise (None, why)."""
     p = ROOT / "profiles" / f"pmc_{config_key}.json"
     if not p.exists():
-        return None
+        return None, {"traffic_source": None}
     try:
-        return json.loads(p.read_text()).get("hbm_bytes_per_launch")
+        d = json.loads(p.read_text())
     except Exception:  # noqa: BLE001
-        return None
+        return None, {"traffic_source": None}
+    prof, cur = d.get("lib_sha16"), lib_sha16()
+    if prof != cur:
+        return None, {"traffic_stale": True, "traffic_profiled_lib": prof, "traffic_this_lib": cur,
+                      "traffic_of_profiled_lib": d.get("hbm_bytes_per_launch")}
+    return d.get("hbm_bytes_per_launch"), {"traffic_stale": False, "traffic_source": f"profiles/pmc_{config_key}.json"}
 
 
 def roofline(c, kern_ms: float, traffic, rank_flops=None, rank_bytes=None):
@@ -218,7 +269,8 @@ def roofline(c, kern_ms: float, traffic, rank_flops=None, rank_bytes=None):
     by = algo_bytes(c) if rank_bytes is None else rank_bytes
     gbs = by / (kern_ms * 1e-3) / 1e9
     tf = fl / (kern_ms * 1e-3) / 1e12
-    base = {"traffic": traffic, "kernel_ms": round(kern_ms, 4), "algorithmic_bytes": by,
+    traffic, prov = traffic if isinstance(traffic, tuple) else (traffic, {})
+    base = {"traffic": traffic, **prov, "kernel_ms": round(kern_ms, 4), "algorithmic_bytes": by,
             "algorithmic_flops": fl}
     if c["Sq"] == 1:
         return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -291,10 +343,16 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--strong", action="store_true", help="split one global problem over the ranks (shard.py)")
+    ap.add_argument("--weak", action="store_true", help="c5: every rank runs its own B1 replica instead")
     ap.add_argument("--global-batch", type=int, default=0, help="--strong: global batch (default: the config's)")
     ap.add_argument("--warmup-seconds", type=float, default=2.0,
                     help="back-to-back op calls before the W warm-up steps (the clock settles)")
     args = ap.parse_args()
+    if args.config == "c5" and not args.weak:
+        # BASELINE C5 is ONE Llama-3-8B attention problem "batch-sharded across 8xMI355X": global batch 8
+        # split into (batch, kv-head) units over the ranks (strong scaling), also at N = 1
+        args.strong = True
+        args.global_batch = args.global_batch or 8
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # not started by torch.distributed.run: start it as a child (never exec) and pass its status on
@@ -320,7 +378,7 @@ def main() -> None:
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
 
-    from flash_attention_cute_amd import flash_attn_func, flash_attn_window_func
+    from flash_attention_cute_amd import flash_attn_func, flash_attn_padded_func, flash_attn_window_func
 
     c = CONFIGS[args.config]
     dt = torch.float16 if c["dtype"] == "fp16" else torch.bfloat16
@@ -355,8 +413,14 @@ def main() -> None:
         k = torch.randn(c["B"], c["Hkv"], c["Sk"], c["D"], device=dev, dtype=dt, generator=gen)
         v = torch.randn(c["B"], c["Hkv"], c["Sk"], c["D"], device=dev, dtype=dt, generator=gen)
         rank_flops, rank_bytes = flops(c), algo_bytes(c)
+        if c.get("lens"):  # padded batch: left padding, sequence b's real keys the last lens[b] positions
+            lens = torch.tensor(c["lens"][:c["B"]], dtype=torch.int32, device=dev)
+            k_end = torch.full_like(lens, c["Sk"])
+            k_start = k_end - lens
 
         def step():
+            if c.get("lens"):
+                return flash_attn_padded_func(q, k, v, k_start, k_end, causal=c["causal"])
             if c.get("W"):
                 return flash_attn_window_func(q, k, v, c["W"] - 1, causal=c["causal"])
             return flash_attn_func(q, k, v, causal=c["causal"])

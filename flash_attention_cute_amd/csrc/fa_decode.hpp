@@ -78,9 +78,16 @@ __global__ __launch_bounds__(256, 1) void fa_decode(const fa_fwd_params p, const
     const int rb = unit % a.n_rb;
     const int hkv = (unit / a.n_rb) % (int)p.num_heads_kv;
     const int b = unit / (a.n_rb * (int)p.num_heads_kv);
-    const int Sq = (int)p.seqlen_q, Sk = (int)p.seqlen_kv, D = (int)p.headdim;
+    const int Sq = (int)p.seqlen_q, D = (int)p.headdim;  // Sq: positions per q-head (row addressing)
     const float sc = p.softmax_scale;
     const float thr_raw = kRescaleThr / sc;
+    // this batch row's keys: absolute rows [k0, k0 + Sk) of k / v (a padded batch's key range,
+    // DecArgs, whose k / v batch strides the host zeroes); else every key
+    int k0 = 0, Sk = (int)p.seqlen_kv;
+    if (a.k_rng) {
+        k0 = a.k_rng[b];
+        Sk = max(a.k_rng[b + a.rng_hi] - k0, 0);
+    }
     const int diag = Sk - Sq;
 
     // this lane's row
@@ -95,9 +102,11 @@ __global__ __launch_bounds__(256, 1) void fa_decode(const fa_fwd_params p, const
     const int per_wave = (s_hi - s_lo + kDecWaves - 1) / kDecWaves;
     const int t_lo = min(s_lo + wave * per_wave, s_hi), t_hi = min(t_lo + per_wave, s_hi);
 
-    const char *kb = (const char *)p.k_ptr + 2 * ((int64_t)b * p.k_batch_stride + (int64_t)hkv * p.k_head_stride);
-    const char *vb = (const char *)p.v_ptr + 2 * ((int64_t)b * p.v_batch_stride + (int64_t)hkv * p.v_head_stride);
     const int ks_ = (int)p.k_seqlen_stride, vs_ = (int)p.v_seqlen_stride;
+    const char *kb = (const char *)p.k_ptr +
+                     2 * ((int64_t)b * p.k_batch_stride + (int64_t)hkv * p.k_head_stride + (int64_t)k0 * ks_);
+    const char *vb = (const char *)p.v_ptr +
+                     2 * ((int64_t)b * p.v_batch_stride + (int64_t)hkv * p.v_head_stride + (int64_t)k0 * vs_);
 
     // ---- LDS-DMA source offsets (lane-linear destination, swizzle on the source) ---------------
     constexpr int ROWS_PER_PIECE = 1024 / RB;

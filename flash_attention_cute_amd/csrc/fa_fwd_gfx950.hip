@@ -42,6 +42,11 @@ fa::Knobs knobs_from_env() {
     if (const char *e = getenv("FA_GFX950_DECODE")) k.decode = strcmp(e, "0") != 0;
     if (const char *e = getenv("FA_DEC_TARGET_WGS")) k.dec_target = atoll(e) > 0 ? atoll(e) : fa::kDecTargetWgs;
     if (const char *e = getenv("FA_DEC_FLAGS")) k.dec_flags = atoi(e);
+    if (k.variant != 0)  // a debug / A-B body replaces the product kernel for the whole process: say so
+        fprintf(stderr,
+                "[fa_gfx950] FA_GFX950_VARIANT=%s: prefill launches run the %s kernel instead of fa_fwd_w4 "
+                "(debug / A-B variant, not the product path)\n",
+                getenv("FA_GFX950_VARIANT"), k.variant == 1 ? "fa_fwd_w8" : k.variant == 2 ? "w4slow" : "fa_fwd_p8");
     return k;
 }
 const fa::Knobs &env_defaults() {
@@ -60,6 +65,8 @@ void fa::set_last_path(int path) { g_last_path = path; }
 // Diagnostic hooks (not in include/fa_gfx950.h; flash_attention_cute_amd/_debug.py):
 // override the knobs for the following launches (a negative value restores that knob's
 // environment/default value) and report the kernel the last call on this thread launched.
+// Single-threaded test hooks: the knobs are plain process-wide fields, so setting them while
+// another thread launches may let that launch see a mix of old and new values.
 extern "C" void fa_debug_set_knobs(int variant, int64_t w4_grid, int decode, int64_t dec_target, int dec_flags) {
     const fa::Knobs &d = env_defaults();
     fa::Knobs &k = knobs_mut();
@@ -103,6 +110,8 @@ using fa::launch_one;
 
 bool aligned16(const void *ptr) { return ((uintptr_t)ptr & 15) == 0; }
 
+constexpr fa::PathArgs kNoPath{nullptr, nullptr, 0, 0, -1, 0, nullptr, nullptr};
+
 int check_params(const fa_fwd_params *p, int dtype, int causal) {
     (void)causal;
     if (!p) return set_err(FA_ERR_INVALID_ARGUMENT, "params is NULL");
@@ -130,10 +139,13 @@ int check_params(const fa_fwd_params *p, int dtype, int causal) {
             return set_err(FA_ERR_INVALID_ARGUMENT, "strides must be multiples of 8 elements (16 bytes)");
     if (p->seqlen_q > 0x3fffffffLL || p->seqlen_kv > 0x3fffffffLL)
         return set_err(FA_ERR_UNSUPPORTED, "sequence lengths must be < 2^30");
-    // 32-bit lane offsets inside one 64-row K/V tile and one 32-row Q/O slab
-    for (int i = 8; i < 12; ++i)
-        if (strides[i] < 0 || strides[i] * 2 * 64 + 256 > 0x7fffffffLL)
+    // 32-bit lane offsets inside one 64-row K/V tile and one wave's Q/O slab: fa_fwd_w4 interleaves
+    // a wave's two 32-row blocks kBlockM / 2 rows apart, so its slab spans kQoSpanRows rows
+    for (int i = 8; i < 12; ++i) {
+        const int64_t rows = (i == 8 || i == 11) ? fa::kQoSpanRows : fa::kBlockN;
+        if (strides[i] < 0 || strides[i] * 2 * rows + 256 > 0x7fffffffLL)
             return set_err(FA_ERR_UNSUPPORTED, "sequence stride too large for 32-bit tile offsets");
+    }
     const int64_t n_qtiles = (p->seqlen_q + fa::kBlockM - 1) / fa::kBlockM;
     const int64_t nwg = n_qtiles * p->num_heads_q * p->batch_size;
     if (nwg > 0x7fffffffLL) return set_err(FA_ERR_UNSUPPORTED, "grid too large (%lld workgroups)", (long long)nwg);
@@ -144,13 +156,12 @@ int check_params(const fa_fwd_params *p, int dtype, int causal) {
 // head-dim dispatch: D <= 64 runs the 64-wide tile, 64 < D <= 128 the 128-wide tile (the reference
 // runs every D <= 128 on its 128 kernel, csrc/kernel_dispatcher.h:45-52)
 template <class DT, bool C>
-int launch(const fa_fwd_params &p, hipStream_t stream, const int *cu_q = nullptr, const int *cu_k = nullptr,
-           const fa::PathArgs &xa = fa::PathArgs{nullptr, nullptr, 0, 0, -1}) {
+int launch(const fa_fwd_params &p, hipStream_t stream, const fa::PathArgs &xa = kNoPath) {
     if (p.headdim <= 64)
-        return p.headdim == 64 ? launch_one<DT, C, 64, true>(p, cu_q, cu_k, xa, stream)
-                               : launch_one<DT, C, 64, false>(p, cu_q, cu_k, xa, stream);
-    return p.headdim == 128 ? launch_one<DT, C, 128, true>(p, cu_q, cu_k, xa, stream)
-                            : launch_one<DT, C, 128, false>(p, cu_q, cu_k, xa, stream);
+        return p.headdim == 64 ? launch_one<DT, C, 64, true>(p, xa, stream)
+                               : launch_one<DT, C, 64, false>(p, xa, stream);
+    return p.headdim == 128 ? launch_one<DT, C, 128, true>(p, xa, stream)
+                            : launch_one<DT, C, 128, false>(p, xa, stream);
 }
 template <class DT, bool C>
 int launch_dec(const fa_fwd_params &p, const fa::DecArgs &a, void *ws, hipStream_t stream) {
@@ -164,7 +175,8 @@ int launch_dec(const fa_fwd_params &p, const fa::DecArgs &a, void *ws, hipStream
 // Split-KV decode path (fa_decode.hpp) for few (q-head, position) rows per (batch, kv-head): the
 // reference's Sq == 1 pack and short GQA query blocks. The `decode` knob (FA_GFX950_DECODE=0) sends
 // them to the prefill kernel instead (A/B measurements).
-bool use_decode(const fa_fwd_params &p) {
+bool use_decode(const fa_fwd_params &p, const fa::PathArgs &ranges = kNoPath) {
+    if (ranges.q_rng) return false;  // query ranges: fa_fwd_w4
     if (!fa::knobs().decode || fa::knobs().variant != 0) return false;
     if (p.head_q_per_group * p.seqlen_q > fa::kDecMaxRows) return false;
     // the row block's q rows are addressed by 32-bit offsets from the group's first q-head
@@ -173,14 +185,18 @@ bool use_decode(const fa_fwd_params &p) {
     return qspan >= 0 && qspan < 0x7ff00000LL;
 }
 
-int dispatch(const fa_fwd_params *params, int dtype, int causal, void *ws, int64_t ws_bytes, void *stream) {
+// ranges: per-sequence query / key ranges (fa_fwd_gfx950_padded), or kNoPath
+int dispatch(const fa_fwd_params *params, int dtype, int causal, void *ws, int64_t ws_bytes, void *stream,
+             const fa::PathArgs &ranges = kNoPath) {
     g_last_path = fa::kPathNone;
     const int rc = check_params(params, dtype, causal);
     if (rc != FA_OK) return rc;
     hipStream_t s = (hipStream_t)stream;
     const fa_fwd_params &p = *params;
-    if (use_decode(p)) {
+    if (use_decode(p, ranges)) {
         fa::DecArgs a = fa::decode_plan(p, ws ? fa::kDecMaxSplit : 1);
+        a.rng_hi = ranges.rng_hi;
+        a.k_rng = ranges.k_rng;
         if (ws && fa::decode_ws_bytes(p, a) > ws_bytes)
             return set_err(FA_ERR_INVALID_ARGUMENT, "workspace of %lld bytes is smaller than the %lld required",
                            (long long)ws_bytes, (long long)fa::decode_ws_bytes(p, a));
@@ -189,8 +205,8 @@ int dispatch(const fa_fwd_params *params, int dtype, int causal, void *ws, int64
         return causal ? launch_dec<fa::BF16, true>(p, a, ws, s) : launch_dec<fa::BF16, false>(p, a, ws, s);
     }
     if (dtype == FA_DTYPE_F16)
-        return causal ? launch<fa::F16, true>(p, s) : launch<fa::F16, false>(p, s);
-    return causal ? launch<fa::BF16, true>(p, s) : launch<fa::BF16, false>(p, s);
+        return causal ? launch<fa::F16, true>(p, s, ranges) : launch<fa::F16, false>(p, s, ranges);
+    return causal ? launch<fa::BF16, true>(p, s, ranges) : launch<fa::BF16, false>(p, s, ranges);
 }
 
 int check_varlen(const fa_varlen_params *v, int dtype, int causal) {
@@ -206,18 +222,91 @@ int check_varlen(const fa_varlen_params *v, int dtype, int causal) {
 }
 
 // window_left >= 0: the local window per sequence (the kernel starts each Q block at its first
-// visible tile; no host cut, the sequence bounds live on the device)
+// visible tile; no host cut, the sequence bounds live on the device). The window is always passed
+// to the kernel: a window longer than a sequence hides nothing there (its per-sequence first tile
+// is 0), so a seqlen_kv below the true maximum cannot drop it.
 int dispatch_varlen(const fa_varlen_params *v, int dtype, int causal, void *stream, int64_t window_left = -1) {
     g_last_path = fa::kPathNone;
     const int rc = check_varlen(v, dtype, causal);
     if (rc != FA_OK) return rc;
+    if (window_left > 0x3fffffffLL) window_left = 0x3fffffff;  // (hides nothing either way)
     hipStream_t s = (hipStream_t)stream;
     const int *cq = v->cu_seqlens_q, *ck = v->cu_seqlens_k;
-    // a window at least as long as every sequence hides nothing (seqlen_kv is the maximum)
-    const fa::PathArgs xa{nullptr, nullptr, 0, 0, window_left < v->base.seqlen_kv ? (int)window_left : -1};
+    // packed rows: sequence b is rows [cu[b], cu[b + 1]) of the tensors, no batch offset
+    fa_fwd_params p = v->base;
+    p.q_batch_stride = p.k_batch_stride = p.v_batch_stride = p.o_batch_stride = 0;
+    const fa::PathArgs xa{nullptr, nullptr, 0, 0, window_left < 0 ? -1 : (int)window_left, 1, cq, ck};
     if (dtype == FA_DTYPE_F16)
-        return causal ? launch<fa::F16, true>(v->base, s, cq, ck, xa) : launch<fa::F16, false>(v->base, s, cq, ck, xa);
-    return causal ? launch<fa::BF16, true>(v->base, s, cq, ck, xa) : launch<fa::BF16, false>(v->base, s, cq, ck, xa);
+        return causal ? launch<fa::F16, true>(p, s, xa) : launch<fa::F16, false>(p, s, xa);
+    return causal ? launch<fa::BF16, true>(p, s, xa) : launch<fa::BF16, false>(p, s, xa);
+}
+
+int check_padded(const fa_padded_params *v, int dtype, int causal) {
+    if (!v) return set_err(FA_ERR_INVALID_ARGUMENT, "params is NULL");
+    if (v->q_range && !v->k_range)
+        return set_err(FA_ERR_INVALID_ARGUMENT, "query ranges need key ranges (pass k starts 0, ends Sk)");
+    if (((uintptr_t)v->q_range & 3) || ((uintptr_t)v->k_range & 3))
+        return set_err(FA_ERR_INVALID_ARGUMENT, "ranges must be 4-byte aligned int32 arrays");
+    if (v->base.batch_size > 0x7fffffffLL) return set_err(FA_ERR_UNSUPPORTED, "batch too large");
+    return check_params(&v->base, dtype, causal);
+}
+
+// Padded batches: per-sequence query / key ranges inside dense tensors. Few rows per kv-head run
+// the split-KV decode kernel (the ranges bound each sequence's key stream), everything else
+// fa_fwd_w4; window_left >= 0 applies the local window per sequence (prefill kernel only).
+// the prefill kernel takes key ranges only together with query ranges: "every query row" of batch
+// row b as absolute rows [b * rows_per_batch, b * rows_per_batch + Sq) (fa_fwd_w4 reads both)
+__global__ void fill_all_rows(int32_t *rng, int batch, int64_t rows_per_batch, int sq) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < batch) {
+        rng[b] = (int32_t)(b * rows_per_batch);
+        rng[batch + b] = (int32_t)(b * rows_per_batch + sq);
+    }
+}
+
+// a padded launch that the prefill kernel serves with key ranges but no query ranges derives the
+// query ranges into the workspace: bytes it needs there (0 if none)
+int64_t padded_qfill_bytes(const fa_padded_params *v, int64_t window_left) {
+    if (!v->k_range || v->q_range) return 0;
+    if (window_left < 0 && use_decode(v->base)) return 0;  // the decode kernel takes key ranges alone
+    return (2 * v->base.batch_size * 4 + 15) / 16 * 16;
+}
+
+int dispatch_padded(const fa_padded_params *v, int dtype, int causal, int64_t window_left, void *ws,
+                    int64_t ws_bytes, void *stream) {
+    g_last_path = fa::kPathNone;
+    const int rc = check_padded(v, dtype, causal);
+    if (rc != FA_OK) return rc;
+    if (window_left > 0x3fffffffLL) window_left = 0x3fffffff;
+    hipStream_t s = (hipStream_t)stream;
+    // ranges hold absolute rows: the batch strides of ranged tensors are not used
+    fa_fwd_params p = v->base;
+    const int32_t *q_range = v->q_range;
+    const int64_t qfill = padded_qfill_bytes(v, window_left);
+    if (qfill > 0) {
+        const fa_fwd_params &b = v->base;
+        if (b.q_seqlen_stride <= 0 || b.q_batch_stride % b.q_seqlen_stride != 0 ||
+            b.o_batch_stride * b.q_seqlen_stride != b.q_batch_stride * b.o_seqlen_stride ||
+            (b.batch_size - 1) * (b.q_batch_stride / b.q_seqlen_stride) + b.seqlen_q > 0x7fffffffLL)
+            return set_err(FA_ERR_INVALID_ARGUMENT,
+                           "without q_range, q and o need batch strides that are equal multiples of their seqlen "
+                           "strides (or pass q_range)");
+        if (!ws || ws_bytes < qfill)
+            return set_err(FA_ERR_INVALID_ARGUMENT, "workspace of %lld bytes is smaller than the %lld required",
+                           (long long)ws_bytes, (long long)qfill);
+        int32_t *qr = (int32_t *)ws;
+        hipLaunchKernelGGL(fill_all_rows, dim3((uint32_t)((b.batch_size + 255) / 256)), dim3(256), 0, s, qr,
+                           (int)b.batch_size, b.q_batch_stride / b.q_seqlen_stride, (int)b.seqlen_q);
+        q_range = qr;
+    }
+    if (v->k_range) p.k_batch_stride = p.v_batch_stride = 0;
+    if (q_range) p.q_batch_stride = p.o_batch_stride = 0;
+    const fa::PathArgs xa{nullptr, nullptr, 0, 0, window_left < 0 ? -1 : (int)window_left, (int)p.batch_size,
+                          q_range, v->k_range};
+    if (window_left < 0) return dispatch(&p, dtype, causal, ws, ws_bytes, stream, xa);
+    if (dtype == FA_DTYPE_F16)
+        return causal ? launch<fa::F16, true>(p, s, xa) : launch<fa::F16, false>(p, s, xa);
+    return causal ? launch<fa::BF16, true>(p, s, xa) : launch<fa::BF16, false>(p, s, xa);
 }
 
 int dispatch_rope(const fa_rope_fwd_params *r, int dtype, int causal, void *stream) {
@@ -230,15 +319,13 @@ int dispatch_rope(const fa_rope_fwd_params *r, int dtype, int causal, void *stre
         return set_err(FA_ERR_UNSUPPORTED, "fused RoPE supports head dim 64 or 128 (got %lld)", (long long)r->base.headdim);
     if (!aligned16(r->rope_cos) || !aligned16(r->rope_sin) || r->rope_batch_stride % 8 || r->rope_seqlen_stride % 8)
         return set_err(FA_ERR_INVALID_ARGUMENT, "RoPE tables must be 16-byte aligned with strides multiple of 8");
-    if (r->rope_seqlen_stride < 0 || r->rope_seqlen_stride * 2 * 64 + 256 > 0x7fffffffLL)
+    if (r->rope_seqlen_stride < 0 || r->rope_seqlen_stride * 2 * fa::kQoSpanRows + 256 > 0x7fffffffLL)
         return set_err(FA_ERR_UNSUPPORTED, "RoPE seqlen stride too large for 32-bit tile offsets");
-    const fa::PathArgs ra{r->rope_cos, r->rope_sin, r->rope_batch_stride, r->rope_seqlen_stride, -1};
+    const fa::PathArgs ra{r->rope_cos, r->rope_sin, r->rope_batch_stride, r->rope_seqlen_stride, -1, 0, nullptr, nullptr};
     hipStream_t s = (hipStream_t)stream;
     if (dtype == FA_DTYPE_F16)
-        return causal ? launch<fa::F16, true>(r->base, s, nullptr, nullptr, ra)
-                      : launch<fa::F16, false>(r->base, s, nullptr, nullptr, ra);
-    return causal ? launch<fa::BF16, true>(r->base, s, nullptr, nullptr, ra)
-                  : launch<fa::BF16, false>(r->base, s, nullptr, nullptr, ra);
+        return causal ? launch<fa::F16, true>(r->base, s, ra) : launch<fa::F16, false>(r->base, s, ra);
+    return causal ? launch<fa::BF16, true>(r->base, s, ra) : launch<fa::BF16, false>(r->base, s, ra);
 }
 
 // Local (sliding) window: keys below the first row's window are cut off the problem (views of k /
@@ -258,11 +345,11 @@ int dispatch_window(const fa_fwd_params *params, int dtype, int causal, int64_t 
     }
     // the last query row's window starts at key Sk' - 1 - window_left: at or before 0, nothing is cut
     if (p.seqlen_kv - 1 <= window_left) return dispatch(&p, dtype, causal, nullptr, 0, stream);
-    const fa::PathArgs xa{nullptr, nullptr, 0, 0, (int)window_left};
+    const fa::PathArgs xa{nullptr, nullptr, 0, 0, (int)window_left, 0, nullptr, nullptr};
     hipStream_t s = (hipStream_t)stream;
     if (dtype == FA_DTYPE_F16)
-        return causal ? launch<fa::F16, true>(p, s, nullptr, nullptr, xa) : launch<fa::F16, false>(p, s, nullptr, nullptr, xa);
-    return causal ? launch<fa::BF16, true>(p, s, nullptr, nullptr, xa) : launch<fa::BF16, false>(p, s, nullptr, nullptr, xa);
+        return causal ? launch<fa::F16, true>(p, s, xa) : launch<fa::F16, false>(p, s, xa);
+    return causal ? launch<fa::BF16, true>(p, s, xa) : launch<fa::BF16, false>(p, s, xa);
 }
 
 }  // namespace
@@ -283,6 +370,21 @@ extern "C" int fa_fwd_gfx950_varlen(const fa_varlen_params *params, int dtype, i
 extern "C" int fa_fwd_gfx950_varlen_window(const fa_varlen_params *params, int dtype, int causal,
                                            int64_t window_left, void *stream) {
     return dispatch_varlen(params, dtype, causal, stream, window_left);
+}
+
+extern "C" int fa_fwd_gfx950_padded(const fa_padded_params *params, int dtype, int causal, int64_t window_left,
+                                    void *workspace, int64_t workspace_bytes, void *stream) {
+    if (workspace && ((uintptr_t)workspace & 15))
+        return set_err(FA_ERR_INVALID_ARGUMENT, "workspace must be 16-byte aligned");
+    return dispatch_padded(params, dtype, causal, window_left, workspace_bytes > 0 ? workspace : nullptr,
+                           workspace_bytes, stream);
+}
+
+extern "C" int64_t fa_fwd_gfx950_padded_workspace_size(const fa_padded_params *params, int dtype, int causal,
+                                                       int64_t window_left) {
+    if (check_padded(params, dtype, causal) != FA_OK) return -1;
+    if (window_left >= 0 || params->q_range || !use_decode(params->base)) return padded_qfill_bytes(params, window_left);
+    return fa::decode_ws_bytes(params->base, fa::decode_plan(params->base, fa::kDecMaxSplit));
 }
 
 extern "C" int fa_fwd_gfx950_varlen_check(const fa_varlen_params *params, int dtype, int causal) {

@@ -216,8 +216,9 @@ __device__ __forceinline__ rsrc_t make_rsrc_u(const char *base, uint32_t nbytes)
     return make_rsrc(ub, __builtin_amdgcn_readfirstlane(nbytes));
 }
 
-// bytes of the first `rows` (<= 64) rows of a [rows, D] slab with row stride `stride` elements;
-// 0 if rows <= 0. The host guarantees 64 * stride * 2 + 256 < 2^31.
+// bytes of the first `rows` rows of a [rows, D] slab with row stride `stride` elements; 0 if
+// rows <= 0. The host guarantees rows * stride * 2 + 256 < 2^31 for the slabs the kernels address
+// (K / V: 64-row tiles; Q / O / RoPE: kQoSpanRows rows, fa_launch.h).
 __device__ __forceinline__ uint32_t slab_bytes(int rows, int stride, int D) {
     return rows <= 0 ? 0u : (uint32_t)(((rows - 1) * stride + D) * 2);
 }
@@ -760,8 +761,7 @@ constexpr int vmcnt_enc(int n) { return (n & 15) | (((n >> 4) & 3) << 14) | 0x70
 // =============================================================================================
 template <class DT, bool kCausal, int kD, bool kExactD>
 __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const int n_qtiles, const int dbg,
-                                                    unsigned long long *stamps, const int *cu_q, const int *cu_k,
-                                                    const PathArgs xa) {
+                                                    unsigned long long *stamps, const PathArgs xa) {
     // Diagnostic build only (-DFA_STAMPS=1, scripts/stamps.py): per-wave s_memtime phase totals.
 #ifdef FA_STAMPS
     unsigned long long st_t0 = __builtin_amdgcn_s_memtime(), st_rt0 = __builtin_amdgcn_s_memrealtime();
@@ -815,6 +815,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // wave's rows span kRowSpan rows from mw
     constexpr int kRowB = kBlockM / 2, kRowSpan = kRowB + 32;
     static_assert(kBlockM == 256, "4 waves x 2 blocks of 32 rows");
+    static_assert(kRowSpan == kQoSpanRows, "the host's 32-bit offset bound (check_params) covers the wave's slab");
     // LDS: K slots 0,1 | V slots 0,1 (64 KiB at D = 128), so every fragment read is a per-lane base
     // plus a 16-bit immediate offset; then (kQL) the Q image, T bytes per wave.
     constexpr int KV0 = 0;
@@ -827,8 +828,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     const int r = lane & 31;
     const int h = lane >> 5;
 
-    // sequence lengths of the current Q block: fixed for a dense launch; per batch row for varlen
-    // (cu_q / cu_k != nullptr: [B + 1] prefix sums, packed rows, p.seqlen_* = the maxima)
+    // sequence lengths of the current Q block: fixed for a dense launch; per batch row with
+    // per-sequence ranges (xa.k_rng != nullptr, PathArgs: packed varlen or padded batches;
+    // p.seqlen_* = upper bounds)
     const int D = (int)p.headdim;
     int Sq = (int)p.seqlen_q, Sk = (int)p.seqlen_kv;
     const float sc = p.softmax_scale;
@@ -864,10 +866,11 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         const int hkv = hq / (int)p.head_q_per_group;
         int64_t qrow0 = (int64_t)b * p.q_batch_stride, krow0 = (int64_t)b * p.k_batch_stride;
         int64_t vrow0 = (int64_t)b * p.v_batch_stride, orow0 = (int64_t)b * p.o_batch_stride;
-        if (cu_q) {  // varlen: batch row b is rows [cu[b], cu[b + 1]) of the packed tensors
-            const int q0 = cu_q[b], k0 = cu_k[b];
-            Sq = cu_q[b + 1] - q0;
-            Sk = cu_k[b + 1] - k0;
+        if (xa.q_rng) {  // this batch row's query rows and keys: absolute rows (the host zeroes the
+                         // batch strides of ranged tensors; both ranges are given together here)
+            const int q0 = xa.q_rng[b], k0 = xa.k_rng[b];
+            Sq = xa.q_rng[b + xa.rng_hi] - q0;
+            Sk = xa.k_rng[b + xa.rng_hi] - k0;
             diag = Sk - Sq;
             n_blocks = (Sk + kBlockN - 1) / kBlockN;
             qrow0 = (int64_t)q0 * p.q_seqlen_stride;
@@ -875,8 +878,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             krow0 = (int64_t)k0 * p.k_seqlen_stride;
             vrow0 = (int64_t)k0 * p.v_seqlen_stride;
         }
-        if (kExactD && xa.cos) {  // (the host only passes RoPE tables to exact-D instantiations)
-            const int64_t crow0 = cu_q ? (int64_t)cu_q[b] * xa.seq_stride : (int64_t)b * xa.batch_stride;
+        if (kExactD && xa.cos) {  // (RoPE: dense launches of exact-D instantiations only)
+            const int64_t crow0 = (int64_t)b * xa.batch_stride;
             cosb = (const char *)xa.cos + 2 * crow0;
             sinb = (const char *)xa.sin + 2 * crow0;
         }
@@ -987,9 +990,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     auto q_rsrc_of = [&](const Work wk) __attribute__((always_inline)) {
         int64_t row0 = (int64_t)wk.b * p.q_batch_stride;
         int sq = (int)p.seqlen_q;
-        if (cu_q) {
-            const int q0 = cu_q[wk.b];
-            sq = cu_q[wk.b + 1] - q0;
+        if (xa.q_rng) {
+            const int q0 = xa.q_rng[wk.b];
+            sq = xa.q_rng[wk.b + xa.rng_hi] - q0;
             row0 = (int64_t)q0 * qs_;
         }
         const int mwn = wk.qtile * kBlockM + wave * 32;
@@ -1551,10 +1554,10 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         if (t + 1 < n_unm) iter(t + 1, IC<1>{}, IC<0>{});
     }
     // causal: the tiles from jA on hold no visible score of any wave's block A (its rows are the
-    // workgroup's first half): they run B only (MASKED 2, then 3)
+    // workgroup's first half, m0 .. m0 + kRowB - 1): they run B only (MASKED 2, then 3)
     int jA = n_loop;
     if (kCausal) {
-        const int x = min(Sk - 1, m0 + kRowSpan - 1 + diag);  // the last visible key of block A
+        const int x = min(Sk - 1, m0 + kRowB - 1 + diag);  // the last visible key of block A
         jA = x < 0 ? 0 : x / kBlockN + 1;
     }
     {
@@ -1716,13 +1719,13 @@ int launch_p8(const fa_fwd_params &p, hipStream_t stream);
 
 // ---- host launch of one instantiation -------------------------------------------------
 template <class DT, bool C, int kD, bool kExact>
-int launch_one(const fa_fwd_params &p, const int *cu_q, const int *cu_k, const PathArgs &xa, hipStream_t stream) {
+int launch_one(const fa_fwd_params &p, const PathArgs &xa, hipStream_t stream) {
     if (xa.cos && !kExact) return set_err(FA_ERR_UNSUPPORTED, "fused RoPE needs head dim 64 or 128");
     const int64_t n_qtiles = (p.seqlen_q + kBlockM - 1) / kBlockM;
     const int64_t nwg = n_qtiles * p.num_heads_q * p.batch_size;
     // varlen, fused RoPE and the local window run fa_fwd_w4 (w4slow under the debug variant); w8 / p8
     // have none of them
-    const bool w4_only = cu_q || xa.cos || xa.window_left >= 0;
+    const bool w4_only = xa.k_rng || xa.cos || xa.window_left >= 0;
     const int variant = w4_only && (variant_from_env() == 1 || variant_from_env() == 3) ? 0 : variant_from_env();
     if (variant == 3) return launch_p8<DT, C, kD, kExact>(p, stream);
     if (variant == 1)
@@ -1731,7 +1734,7 @@ int launch_one(const fa_fwd_params &p, const int *cu_q, const int *cu_k, const P
     else
         // persistent: about one workgroup per CU (the kernel walks the Q blocks itself)
         hipLaunchKernelGGL((fa_fwd_w4<DT, C, kD, kExact>), dim3((uint32_t)w4_grid(nwg)), dim3(256), 0, stream, p,
-                           (int)n_qtiles, variant == 2 ? 1 : 0, stamp_buffer(), cu_q, cu_k, xa);
+                           (int)n_qtiles, variant == 2 ? 1 : 0, stamp_buffer(), xa);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "HIP launch failed: %s", hipGetErrorString(e));
     set_last_path(variant == 1 ? kPathW8 : variant == 2 ? kPathW4Slow : kPathW4);

@@ -11,7 +11,7 @@
 #include "fa_launch.h"
 namespace fa {
 template <class DT, bool C, int kD, bool kExact>
-int launch_one(const fa_fwd_params &, const int *, const int *, const PathArgs &, hipStream_t) { return set_err(FA_ERR_UNSUPPORTED, "stub instantiation"); }
+int launch_one(const fa_fwd_params &, const PathArgs &, hipStream_t) { return set_err(FA_ERR_UNSUPPORTED, "stub instantiation"); }
 template <class DT, bool C, int kD, bool kExact>
 int launch_decode(const fa_fwd_params &, DecArgs, void *, hipStream_t) {
     return set_err(FA_ERR_UNSUPPORTED, "stub instantiation");
@@ -25,7 +25,6 @@ int launch_decode(const fa_fwd_params &, DecArgs, void *, hipStream_t) {
 
 namespace fa {
 template int launch_one<FA_INST_DT, (FA_INST_CAUSAL != 0), FA_INST_D, (FA_INST_EXACT != 0)>(const fa_fwd_params &,
-                                                                                        const int *, const int *,
                                                                                         const PathArgs &, hipStream_t);
 template int launch_decode<FA_INST_DT, (FA_INST_CAUSAL != 0), FA_INST_D, (FA_INST_EXACT != 0)>(const fa_fwd_params &,
                                                                                            DecArgs, void *,

@@ -14,6 +14,10 @@ namespace fa {
 
 constexpr int kBlockM = 256;  // query rows per workgroup
 constexpr int kBlockN = 64;   // keys per KV tile
+// rows one wave's Q / O (and RoPE table) slab spans in fa_fwd_w4: block A's 32 rows, block B's
+// 32 rows kBlockM / 2 rows later; the host bounds q / o / RoPE seqlen strides so that a slab's
+// byte offsets fit 32 bits (check_params)
+constexpr int kQoSpanRows = kBlockM / 2 + 32;
 constexpr int kWaves = 8;     // fa_fwd_w8
 constexpr int kThreads = kWaves * 64;
 
@@ -64,18 +68,25 @@ int64_t w4_grid(int64_t nwg);
 // Local window (fa_fwd_gfx950_window): key n is visible to query m only if n >= m + Sk - Sq -
 // window_left (the sliding window of window_left + 1 keys ending at the bottom-right diagonal);
 // window_left < 0: none.
+// Per-sequence ranges (device int32 arrays, or nullptr = the whole dimension): batch row b's query
+// rows are [q_rng[b], q_rng[b + rng_hi]) and its keys [k_rng[b], k_rng[b + rng_hi]), ABSOLUTE rows
+// (row r at base + r * seqlen stride; the host zeroes the batch strides of ranged tensors); query
+// ranges come with key ranges. Packed varlen passes cu_seqlens with rng_hi = 1
+// (fa_fwd_gfx950_varlen); padded batches [2, B] arrays of starts then ends with rng_hi = B
+// (fa_fwd_gfx950_padded). Masks are bottom-right aligned per sequence.
 struct PathArgs {
     const void *cos;
     const void *sin;
     int64_t batch_stride;
     int64_t seq_stride;
     int window_left;
+    int rng_hi;
+    const int *q_rng, *k_rng;
 };
 
-// launch one (dtype, causal, head-dim tile, exact head dim) instantiation on `stream`; cu_q / cu_k
-// (device, [B + 1] prefix sums of the per-sequence lengths) select the varlen layout, or nullptr
+// launch one (dtype, causal, head-dim tile, exact head dim) instantiation on `stream`
 template <class DT, bool C, int kD, bool kExact>
-int launch_one(const fa_fwd_params &p, const int *cu_q, const int *cu_k, const PathArgs &xa, hipStream_t stream);
+int launch_one(const fa_fwd_params &p, const PathArgs &xa, hipStream_t stream);
 
 
 // ---- split-KV decode (fa_decode.hpp) -------------------------------------------------------------
@@ -100,6 +111,11 @@ struct DecArgs {
     float *ws_o;    // [units * n_split][32][kD] fp32 partial O / l    (n_split > 1)
     float *ws_lse;  // [units * n_split][32] fp32 m * s' + log2(l)      (n_split > 1)
     int flags;      // kDec* bits
+    // per-sequence key ranges (PathArgs: absolute rows [k_rng[b], k_rng[b + rng_hi]) of k / v, whose
+    // batch strides the host zeroes), or nullptr (every key). Query ranges are not supported here
+    // (the dispatcher sends them to fa_fwd_w4).
+    int rng_hi;
+    const int *k_rng;
 };
 constexpr int kDecNt = 1;  // K/V LDS-DMA with the non-temporal cache policy
 
@@ -146,8 +162,7 @@ int launch_decode(const fa_fwd_params &p, DecArgs a, void *ws, hipStream_t strea
     X(BF16, true, 128, false) X(BF16, true, 128, true)
 
 #define FA_DECLARE_EXTERN(DT, C, D, E)                                                  \
-    extern template int launch_one<DT, C, D, E>(const fa_fwd_params &, const int *, const int *, const PathArgs &, \
-                                                hipStream_t);                                                 \
+    extern template int launch_one<DT, C, D, E>(const fa_fwd_params &, const PathArgs &, hipStream_t);            \
     extern template int launch_decode<DT, C, D, E>(const fa_fwd_params &, DecArgs, void *, hipStream_t);
 FA_FOR_EACH_INSTANCE(FA_DECLARE_EXTERN)
 #undef FA_DECLARE_EXTERN

@@ -16,6 +16,7 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <cmath>
 #include <mutex>
 #include <string>
@@ -416,6 +417,142 @@ torch::Tensor flash_attention_varlen_fwd(torch::Tensor &q, torch::Tensor &k, tor
     return o;
 }
 
+// Padded batches (include/fa_gfx950.h fa_fwd_gfx950_padded): dense q [B, Hq, Sq, D], k / v
+// [B, Hkv, Sk, D] (any strides, last dim contiguous) with the real tokens of batch row b at key
+// positions [k_start[b], k_end[b]) and, optionally, query positions [q_start[b], q_end[b]) -- int32
+// [B] on the device. Read in place: no packing copy, no host synchronisation (graph-capturable).
+// Output rows outside the query ranges are 0. Sq == 1 without query ranges takes the q-head pack
+// and the split-KV decode kernel over each sequence's key range (a window there narrows the key
+// range on the device instead). No reference counterpart (the reference drops attention_mask).
+torch::Tensor flash_attention_padded_fwd(torch::Tensor &q, torch::Tensor &k, torch::Tensor &v,
+                                         c10::optional<torch::Tensor> q_start, c10::optional<torch::Tensor> q_end,
+                                         torch::Tensor &k_start, torch::Tensor &k_end, float softmax_scale,
+                                         bool causal, int64_t window_left) {
+    TORCH_CHECK(q.dim() == 4 && k.dim() == 4 && v.dim() == 4, "q, k, v must be 4-D [batch, heads, seqlen, dim]");
+    TORCH_CHECK(q.size(0) == k.size(0) && q.size(0) == v.size(0), "q, k, v must have the same batch size");
+    TORCH_CHECK(k.size(1) == v.size(1), "k, v must have the same number of heads");
+    TORCH_CHECK(k.size(2) == v.size(2), "k, v must have the same sequence length");
+    TORCH_CHECK(q.size(3) == k.size(3) && q.size(3) == v.size(3), "q, k, v must have the same hidden dimension");
+    TORCH_CHECK(q.size(0) > 0 && q.size(1) > 0 && q.size(2) > 0 && q.size(3) > 0 && k.size(2) > 0,
+                "q, k, v must have at least one element");
+    TORCH_CHECK(q.size(1) % k.size(1) == 0, "number of heads in q must be multiple of number of heads in k and v");
+    TORCH_CHECK(q.dtype() == k.dtype() && q.dtype() == v.dtype(), "q, k, v must have the same data type");
+    TORCH_CHECK(q.dtype() == torch::kHalf || q.dtype() == torch::kBFloat16,
+                "q, k, v only support fp16 or bf16 data type");
+    TORCH_CHECK(q.stride(3) == 1 && k.stride(3) == 1 && v.stride(3) == 1,
+                "q, k, v must be contiguous in the last dimension");
+    TORCH_CHECK(q.size(3) % 8 == 0, "hidden dimension must be multiple of 8");
+    TORCH_CHECK(q.size(3) <= 128, "only support hidden dimension <= 128");
+    TORCH_CHECK(q.is_cuda() && k.is_cuda() && v.is_cuda(), "q, k, v must be on CUDA device");
+    TORCH_CHECK(q.device() == k.device() && q.device() == v.device(), "q, k, v must be on the same CUDA device");
+    TORCH_CHECK(q_start.has_value() == q_end.has_value(), "q_start and q_end must be given together");
+    const int64_t bs = q.size(0);
+    auto check_range = [&](const torch::Tensor &t, const char *name) {
+        TORCH_CHECK(t.dtype() == torch::kInt32 && t.dim() == 1 && t.size(0) == bs, name, " must be int32 [batch]");
+        TORCH_CHECK(t.device() == q.device(), name, " must be on the device of q");
+    };
+    check_range(k_start, "k_start");
+    check_range(k_end, "k_end");
+    const bool q_ranges = q_start.has_value();
+    if (q_ranges) {
+        check_range(*q_start, "q_start");
+        check_range(*q_end, "q_end");
+    }
+    c10::DeviceGuard device_guard(q.device());
+    TORCH_CHECK(device_is_gfx950(q.device().index()),
+                "flash attention (gfx950 build) is only supported on MI355X / gfx950 devices");
+
+    // the kernels address a ranged tensor by absolute rows (row r at base + r * seqlen stride): the
+    // batch stride must be a multiple of the seqlen stride, the same multiple for k and v (q and o)
+    auto rows_per_batch = [](const torch::Tensor &t) -> int64_t {
+        if (t.size(0) == 1) return 0;
+        if (t.stride(2) <= 0 || t.stride(0) % t.stride(2) != 0) return -1;
+        return t.stride(0) / t.stride(2);
+    };
+    torch::Tensor qx = aligned16(q) ? q : q.contiguous();
+    torch::Tensor kx = aligned16(k) ? k : k.contiguous();
+    torch::Tensor vx = aligned16(v) ? v : v.contiguous();
+    if (rows_per_batch(kx) < 0 || rows_per_batch(kx) != rows_per_batch(vx) || kx.stride(2) != vx.stride(2)) {
+        kx = kx.contiguous();
+        vx = vx.contiguous();
+    }
+    int64_t head_q = qx.size(1), seqlen_q = qx.size(2);
+    const int64_t head_kv = kx.size(1), headdim = qx.size(3), g = head_q / head_kv;
+    torch::Tensor ks = k_start, ke = k_end;
+    // decode: one query row that sees the last window_left + 1 keys of its range -> narrow the range
+    if (window_left >= 0 && seqlen_q == 1 && !q_ranges) {
+        ks = torch::maximum(ks, ke - (int32_t)std::min<int64_t>(window_left + 1, 0x7fffffff));
+        window_left = -1;
+    }
+    // Sq == 1: the q-head pack of flash_attention_fwd (reference :64-83)
+    const bool pack = seqlen_q == 1 && !q_ranges && window_left < 0;
+    if (pack) {
+        head_q = head_kv;
+        seqlen_q = g;
+        causal = false;
+        qx = qx.reshape({bs, head_q, seqlen_q, headdim});
+        if (!aligned16(qx)) qx = qx.contiguous();
+    }
+    if (q_ranges && rows_per_batch(qx) < 0) qx = qx.contiguous();
+    auto o = torch::empty_like(qx);
+    if (!aligned16(o) || o.strides() != qx.strides()) o = torch::empty(qx.sizes(), qx.options());
+    if (q_ranges) o.zero_();  // rows outside the query ranges are not written by the kernel
+
+    // [2, B] absolute rows: starts, then ends
+    const auto batch_idx = torch::arange(bs, k_start.options());
+    const int64_t rk = rows_per_batch(kx);
+    torch::Tensor k_range = torch::cat({ks + batch_idx * (int32_t)rk, ke + batch_idx * (int32_t)rk}).contiguous();
+    torch::Tensor q_range;
+    if (q_ranges) {
+        const int64_t rq = rows_per_batch(qx);
+        TORCH_CHECK(rows_per_batch(o) == rq, "internal: o rows differ from q rows");
+        q_range = torch::cat({*q_start + batch_idx * (int32_t)rq, *q_end + batch_idx * (int32_t)rq}).contiguous();
+    }
+
+    fa_padded_params pp;
+    fa_fwd_params &params = pp.base;
+    params.q_ptr = qx.data_ptr();
+    params.k_ptr = kx.data_ptr();
+    params.v_ptr = vx.data_ptr();
+    params.o_ptr = o.data_ptr();
+    params.batch_size = bs;
+    params.num_heads_q = head_q;
+    params.num_heads_kv = head_kv;
+    params.seqlen_q = seqlen_q;
+    params.seqlen_kv = kx.size(2);
+    params.headdim = headdim;
+    params.head_q_per_group = pack ? 1 : g;
+    params.q_batch_stride = stride_or_zero(qx, 0);
+    params.k_batch_stride = stride_or_zero(kx, 0);
+    params.v_batch_stride = stride_or_zero(vx, 0);
+    params.o_batch_stride = stride_or_zero(o, 0);
+    params.q_head_stride = stride_or_zero(qx, 1);
+    params.k_head_stride = stride_or_zero(kx, 1);
+    params.v_head_stride = stride_or_zero(vx, 1);
+    params.o_head_stride = stride_or_zero(o, 1);
+    // ranged tensors keep their seqlen stride even at size 1 (it converts rows into addresses)
+    params.q_seqlen_stride = q_ranges ? qx.stride(2) : stride_or_zero(qx, 2);
+    params.k_seqlen_stride = kx.stride(2);
+    params.v_seqlen_stride = vx.stride(2);
+    params.o_seqlen_stride = q_ranges ? o.stride(2) : stride_or_zero(o, 2);
+    softmax_scale *= M_LOG2E;
+    params.softmax_scale = softmax_scale;
+    pp.q_range = q_ranges ? q_range.data_ptr<int32_t>() : nullptr;
+    pp.k_range = k_range.data_ptr<int32_t>();
+
+    const int dtype = qx.scalar_type() == torch::kHalf ? FA_DTYPE_F16 : FA_DTYPE_BF16;
+    void *stream = c10::hip::getCurrentHIPStream(qx.device().index()).stream();
+    const int64_t ws_bytes = fa_fwd_gfx950_padded_workspace_size(&pp, dtype, causal ? 1 : 0, window_left);
+    TORCH_CHECK(ws_bytes >= 0, "fa_fwd_gfx950_padded_workspace_size failed: ", fa_last_error());
+    torch::Tensor ws;
+    if (ws_bytes > 0) ws = torch::empty({ws_bytes}, qx.options().dtype(torch::kUInt8));
+    const int rc = fa_fwd_gfx950_padded(&pp, dtype, causal ? 1 : 0, window_left,
+                                        ws_bytes > 0 ? ws.data_ptr() : nullptr, ws_bytes, stream);
+    TORCH_CHECK(rc == FA_OK, "fa_fwd_gfx950_padded failed (code ", rc, "): ", fa_last_error());
+    if (o.sizes() != q.sizes()) o = o.reshape(q.sizes());
+    return o;
+}
+
 }  // namespace flash_attention
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -427,6 +564,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           "FlashAttention-2 forward with rotate-half RoPE applied to q in the kernel's Q load, gfx950");
     m.def("flash_attention_window_fwd", &flash_attention::flash_attention_window_fwd,
           "FlashAttention-2 forward with a local (sliding) window of window_left + 1 keys, gfx950");
+    m.def("flash_attention_padded_fwd", &flash_attention::flash_attention_padded_fwd,
+          "FlashAttention-2 forward over padded batches (per-sequence query / key ranges in dense tensors), gfx950");
     m.def("rope_apply", &flash_attention::rope_apply, "rotate-half RoPE, one HIP pass (gfx950)");
     m.def("abi_version", []() { return fa_abi_version(); });
 }

@@ -23,6 +23,7 @@ same registrations (CPU default, "cuda" kernel, fake) and the same pad / contigu
 from __future__ import annotations
 
 import warnings
+from typing import Optional
 
 import torch
 
@@ -157,6 +158,87 @@ def flash_attn_varlen_func(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, ma
     softmax_scale = (q.size(-1) ** -0.5) if softmax_scale is None else softmax_scale
     return torch.ops.flash_attention.varlen_forward(q, k, v, cu_seqlens_q, cu_seqlens_k, int(max_seqlen_q),
                                                     int(max_seqlen_k), softmax_scale, causal, int(window_left))
+
+
+# ---------------------------------------------------------------------------------------------
+# padded batches -- per-sequence ranges inside dense tensors (include/fa_gfx950.h
+# fa_fwd_gfx950_padded); no reference counterpart (the reference drops attention_mask,
+# models/rope_attn_fwd.py:40-64). An HF left / right padding mask is lowered to this: the KV cache
+# and the projections are read in place, decode steps keep the q-head pack and split-KV kernel.
+# ---------------------------------------------------------------------------------------------
+@torch.library.custom_op("flash_attention::padded_forward", mutates_args=())
+def flash_attention_padded_forward(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, k_start: torch.Tensor,
+                                   k_end: torch.Tensor, q_start: Optional[torch.Tensor] = None,
+                                   q_end: Optional[torch.Tensor] = None, softmax_scale: float = None,
+                                   causal: bool = False, window_left: int = -1) -> torch.Tensor:
+    # q: [B, Hq, Sq, D]; k, v: [B, Hkv, Sk, D]; batch row b's keys are positions [k_start[b], k_end[b])
+    # and (optional) its queries [q_start[b], q_end[b]). Non-GPU default: per-sequence torch SDPA with
+    # the kernel's semantics (bottom-right causal per sequence, GQA, rows outside / with no key 0).
+    warnings.warn("Flash Attention only support cuda now, fallback to pytorch implementation.", stacklevel=2)
+    out = torch.zeros_like(q)
+    sq = q.size(2)
+    ks, ke = k_start.tolist(), k_end.tolist()
+    qs = q_start.tolist() if q_start is not None else [0] * q.size(0)
+    qe = q_end.tolist() if q_end is not None else [sq] * q.size(0)
+    for b in range(q.size(0)):
+        q0, q1, k0, k1 = qs[b], qe[b], ks[b], ke[b]
+        if q1 <= q0 or k1 <= k0:
+            continue
+        if window_left >= 0:
+            mask = _window_mask(q1 - q0, k1 - k0, window_left, causal, q.device)
+        else:
+            # bottom-right per sequence (one query row sees every key, as the Sq == 1 pack's non-causal)
+            mask = _bottom_right_causal(q1 - q0, k1 - k0, q.device) if causal else None
+        o = torch.nn.functional.scaled_dot_product_attention(q[b:b + 1, :, q0:q1], k[b:b + 1, :, k0:k1],
+                                                             v[b:b + 1, :, k0:k1], attn_mask=mask,
+                                                             scale=softmax_scale, enable_gqa=True)
+        if mask is not None:
+            o = o.masked_fill(~mask.any(dim=1)[None, None, :, None], 0)
+        out[b:b + 1, :, q0:q1] = o
+    return out
+
+
+@torch.library.register_kernel("flash_attention::padded_forward", "cuda")
+def flash_attention_padded_forward_cuda(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, k_start: torch.Tensor,
+                                        k_end: torch.Tensor, q_start: Optional[torch.Tensor] = None,
+                                        q_end: Optional[torch.Tensor] = None, softmax_scale: float = None,
+                                        causal: bool = False, window_left: int = -1) -> torch.Tensor:
+    if flash_attention_cuda is None:
+        raise RuntimeError(f"gfx950 flash attention extension is not available: {_load_error!r}")
+    head_dim = q.size(3)
+    need_padding = head_dim % 8 != 0
+    if need_padding:
+        pad = [0, 8 - head_dim % 8]
+        q = torch.nn.functional.pad(q, pad)
+        k = torch.nn.functional.pad(k, pad)
+        v = torch.nn.functional.pad(v, pad)
+    q = q.contiguous() if q.stride(3) != 1 else q
+    k = k.contiguous() if k.stride(3) != 1 else k
+    v = v.contiguous() if v.stride(3) != 1 else v
+    attn = flash_attention_cuda.flash_attention_padded_fwd(q, k, v, q_start, q_end, k_start, k_end, softmax_scale,
+                                                           causal, int(window_left))
+    if need_padding:
+        attn = attn[:, :, :, :head_dim]
+    return attn
+
+
+@torch.library.register_fake("flash_attention::padded_forward")
+def flash_attention_padded_forward_fake(q, k, v, k_start, k_end, q_start=None, q_end=None, softmax_scale=None,
+                                        causal=False, window_left=-1):
+    return torch.empty_like(q)
+
+
+def flash_attn_padded_func(q, k, v, k_start, k_end, q_start=None, q_end=None, softmax_scale=None, causal=False,
+                           window_left=-1):
+    """Attention over a padded batch read in place: q [B, Hq, Sq, D], k / v [B, Hkv, Sk, D] (any strides,
+    e.g. HF projection views and the KV cache), batch row b's real keys at positions
+    ``[k_start[b], k_end[b])`` and, optionally, its real queries at ``[q_start[b], q_end[b])`` (int32 [B]
+    on q's device; default: every query row). Causal / window masks are bottom-right aligned per
+    sequence; output rows outside the query ranges are 0. No host synchronisation (graph-capturable);
+    Sq == 1 takes the q-head pack and the split-KV decode kernel."""
+    softmax_scale = (q.size(-1) ** -0.5) if softmax_scale is None else softmax_scale
+    return torch.ops.flash_attention.padded_forward(q, k, v, k_start, k_end, q_start, q_end, softmax_scale, causal,
+                                                    int(window_left))
 
 
 # ---------------------------------------------------------------------------------------------

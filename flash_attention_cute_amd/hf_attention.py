@@ -28,14 +28,21 @@ from typing import Optional, Tuple
 import torch
 from torch import nn
 
-from .flash_attention import (_bottom_right_causal, _window_mask, apply_rope, flash_attn_func, flash_attn_rope_func,
-                              flash_attn_varlen_func, flash_attn_window_func)
+from .flash_attention import (_bottom_right_causal, _window_mask, apply_rope, flash_attn_func, flash_attn_padded_func,
+                              flash_attn_rope_func, flash_attn_varlen_func, flash_attn_window_func)
 
 # On GPU tensors the patched forward rotates k with one HIP pass (apply_rope) and q inside the
 # attention kernel (flash_attn_rope_func) instead of the reference's elementwise torch ops
 # (reference models/rope_attn_fwd.py:14-38). False restores the reference's order of operations
 # (A/B measurements, scripts/benchmark_llm.py --no-fused-rope).
 FUSE_ROPE = True
+
+# Attention masks are validated on the host by default (a mask this lowering cannot express raises
+# instead of being ignored), which costs host synchronisations. True TRUSTS the mask to be causal +
+# key padding with each sequence's real tokens one contiguous run (left or right padding, what
+# ``generate`` builds): the padded path then runs without any host synchronisation, so a decode
+# step can be captured in a HIP graph.
+TRUST_PADDING_MASK = False
 
 
 def rotate_half(x: torch.Tensor) -> torch.Tensor:
@@ -68,6 +75,11 @@ def key_padding(attention_mask: Optional[torch.Tensor], sq: int, sk: int, causal
     """
     if attention_mask is None:
         return None
+    if TRUST_PADDING_MASK:  # no validation, no host synchronisation
+        m = attention_mask
+        if m.dim() == 4:
+            return (m[:, 0] if m.dtype == torch.bool else (m[:, 0] == 0)).any(dim=1)
+        return m.bool()
     if sq > sk:
         raise NotImplementedError("flash_attention_cute_amd: attention_mask with more queries than keys")
     m = attention_mask
@@ -114,6 +126,38 @@ def key_padding(attention_mask: Optional[torch.Tensor], sq: int, sk: int, causal
     return kv_valid
 
 
+def padding_ranges(kv_valid: torch.Tensor, sq: int, check: bool = True):
+    """[B, Sk] per-token validity -> int32 device tensors (k_start, k_end, q_start, q_end): batch row b's
+    real keys are positions [k_start, k_end) and its real queries (the last Sq token positions) rows
+    [q_start, q_end). None when some row's real tokens are not one contiguous run (``check``: one host
+    synchronisation; check=False trusts the mask)."""
+    sk = kv_valid.shape[1]
+    idx = torch.arange(sk, device=kv_valid.device, dtype=torch.int32)[None]
+    cnt = kv_valid.sum(1, dtype=torch.int32)
+    first = torch.where(kv_valid, idx, sk).amin(1)
+    if check:
+        last = torch.where(kv_valid, idx, -1).amax(1)
+        if bool(((last - first + 1 != cnt) & (cnt > 0)).any()):
+            return None
+    k_start = torch.where(cnt > 0, first, 0).to(torch.int32)
+    k_end = k_start + cnt
+    off = sk - sq  # query row i is token position off + i
+    q_start = (k_start - off).clamp(0, sq).to(torch.int32)
+    q_end = (k_end - off).clamp(0, sq).to(torch.int32)
+    return k_start, k_end, q_start, q_end
+
+
+def _padded_attention(query, key, value, ranges, causal, scaling, window_left=-1):
+    """Padded batch read in place (``flash_attn_padded_func``) -> [B, Sq, Hq, D], padding rows 0. A decode
+    step (Sq == 1) passes no query ranges, so it keeps the q-head pack and the split-KV kernel."""
+    k_start, k_end, q_start, q_end = ranges
+    if query.shape[2] == 1:
+        q_start = q_end = None
+    o = flash_attn_padded_func(query, key, value, k_start, k_end, q_start, q_end, softmax_scale=scaling,
+                               causal=causal, window_left=window_left)
+    return o.transpose(1, 2)
+
+
 def _varlen_attention(query, key, value, kv_valid, causal, scaling, window_left=-1):
     """Padded batch -> packed sequences -> ``flash_attn_varlen_func`` -> padded [B, Sq, Hq, D] (padding
     rows 0). q/k/v are [B, H, S, D] views; the valid query rows are the last Sq token positions."""
@@ -142,8 +186,10 @@ def _flash_attention_forward(module: nn.Module, query: torch.Tensor, key: torch.
                              softcap: Optional[float] = None, **kwargs) -> Tuple[torch.Tensor, None]:
     """Attention core (reference models/rope_attn_fwd.py:40-64): returns [B, Sq, Hq, D], None.
 
-    Unlike the reference, ``attention_mask`` is honoured: a padding mask runs the varlen kernel
-    over the packed real tokens (``key_padding``); masks it cannot express raise."""
+    Unlike the reference, ``attention_mask`` is honoured: a padding mask whose real tokens form one
+    run per sequence (left / right padding) runs the padded kernel on the tensors in place
+    (``padding_ranges``); other padding is packed for the varlen kernel (``key_padding``); masks it
+    cannot express raise."""
     kwargs.pop("is_causal", None)
     if softcap is not None:
         raise NotImplementedError("flash_attention_cute_amd: attention logit softcapping is not supported")
@@ -159,8 +205,11 @@ def _flash_attention_forward(module: nn.Module, query: torch.Tensor, key: torch.
     if kv_valid is not None:
         if rope is not None:
             query = apply_rope(query, *rope)
-        return _varlen_attention(query, key, value, kv_valid, causal, scaling,
-                                 -1 if window_left is None else window_left), None
+        wl = -1 if window_left is None else window_left
+        ranges = padding_ranges(kv_valid, sq, check=not TRUST_PADDING_MASK)
+        if ranges is not None:
+            return _padded_attention(query, key, value, ranges, causal, scaling, wl), None
+        return _varlen_attention(query, key, value, kv_valid, causal, scaling, wl), None
     if window_left is not None:
         if rope is not None:
             query = apply_rope(query, *rope)

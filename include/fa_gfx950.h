@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define FA_GFX950_ABI_VERSION 5
+#define FA_GFX950_ABI_VERSION 6
 
 /* Field order mirrors reference csrc/flash_attention.h:5-37. */
 typedef struct fa_fwd_params {
@@ -150,8 +150,9 @@ int fa_fwd_gfx950_geometry(const fa_fwd_params *params, int causal, int64_t *blo
  * o [total_q, Hq, D] (any row / head strides, multiples of 8 elements; last dim contiguous).
  * Sequence b owns q rows [cu_seqlens_q[b], cu_seqlens_q[b+1]) and k/v rows
  * [cu_seqlens_k[b], cu_seqlens_k[b+1]) -- int32 prefix sums in DEVICE memory, B + 1 entries.
- * In `base`: batch_size = B; seqlen_q / seqlen_kv = the maximum per-sequence lengths (seqlen_q sizes
- * the grid: a longer sequence would be cut short, so the caller must pass the true maximum);
+ * In `base`: batch_size = B; seqlen_q / seqlen_kv = upper bounds of the per-sequence lengths
+ * (seqlen_q sizes the grid: a longer sequence would be cut short, so it must be at least the true
+ * maximum; a larger bound only launches empty q-tiles);
  * the *_batch_stride fields are ignored; the head / seqlen strides are those of the packed tensors.
  * Causal masking is bottom-right aligned per sequence (key n visible to query m iff
  * n <= m + Sk_b - Sq_b), rows of a sequence with no visible key are 0, a sequence with Sk_b == 0
@@ -172,6 +173,43 @@ int fa_fwd_gfx950_varlen_window(const fa_varlen_params *params, int dtype, int c
 
 /* Host-only validation of the varlen parameters (the device arrays are not read). */
 int fa_fwd_gfx950_varlen_check(const fa_varlen_params *params, int dtype, int causal);
+
+/*
+ * Padded batches: per-sequence query / key ranges inside DENSE tensors (the layout of an HF
+ * padded batch and its KV cache, read in place -- no packing copy). No reference counterpart
+ * (the reference drops attention_mask, models/rope_attn_fwd.py:40-64); this is the entry an HF
+ * left- or right-padding mask is lowered to.
+ *
+ * `base` describes dense q [B, Hq, Sq, D], k/v [B, Hkv, Sk, D], o [B, Hq, Sq, D] as for
+ * fa_fwd_gfx950 (seqlen_q / seqlen_kv = the padded lengths). Sequence b's real keys are ROWS
+ * [k_range[b], k_range[B + b]) of k and v, counted from the base pointer in units of the seqlen
+ * stride (row r of kv-head h at k_ptr + h * k_head_stride + r * k_seqlen_stride; for a tensor
+ * whose batch stride is S times its seqlen stride, position s of batch row b is row b * S + s),
+ * and its real queries rows [q_range[b], q_range[B + b]) of q and o likewise -- int32 [2, B] arrays
+ * (B starts, then B ends) in DEVICE memory. The batch strides of a ranged tensor are not used.
+ * q_range == NULL: every query row of batch row b (q / o batch strides apply); k_range == NULL:
+ * every key (query ranges need key ranges). Masks are bottom-right aligned per sequence (key n of
+ * the range visible to query m of the range iff n - k_start <= m - q_start + Sk_b - Sq_b);
+ * window_left >= 0 adds the local window of fa_fwd_gfx950_window per sequence (< 0: none).
+ * Output rows outside the query ranges are NOT written (the torch binding zero-fills them first);
+ * rows with no visible key are 0. Few query rows per kv-head without query ranges or window (Sq ==
+ * 1 after the q-head pack, or head_q_per_group * Sq <= 64) run the split-KV decode kernel on each
+ * sequence's key rows, which wants fa_fwd_gfx950_padded_workspace_size() bytes of workspace to
+ * split (NULL: unsplit), as fa_fwd_gfx950_ws. Asynchronous, no host synchronisation: safe under
+ * hipGraph capture.
+ */
+typedef struct fa_padded_params {
+    fa_fwd_params base;
+    const int32_t *q_range; /* [2, B] first rows then end rows, device, or NULL */
+    const int32_t *k_range; /* [2, B] first rows then end rows, device, or NULL */
+} fa_padded_params;
+
+int fa_fwd_gfx950_padded(const fa_padded_params *params, int dtype, int causal, int64_t window_left,
+                         void *workspace, int64_t workspace_bytes, void *stream);
+
+/* Workspace bytes fa_fwd_gfx950_padded wants (0: no split; -1: invalid parameters). Host-only. */
+int64_t fa_fwd_gfx950_padded_workspace_size(const fa_padded_params *params, int dtype, int causal,
+                                            int64_t window_left);
 
 /*
  * RoPE fused into the attention forward (the reference applies RoPE with

@@ -1,5 +1,5 @@
 #!/bin/bash
-# usage: bash scripts/dev/ab_run.sh "c2 c4 c5" lib1.so lib2.so ...   (interleaved A/B of library builds)
+# usage: bash scripts/experiments/ab_run.sh "c2 c4 c5" lib1.so lib2.so ...   (interleaved A/B of library builds)
 set -o pipefail
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
 CFGS=$1; shift

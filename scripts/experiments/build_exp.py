@@ -1,5 +1,5 @@
 """Build tagged stamps/experiment variants of the ABI library (only the instantiations that
-scripts/stamps.py c2 / c4 run). usage: python scripts/dev/build_exp.py tag[:DEF1,DEF2][:flag flag] ..."""
+scripts/stamps.py c2 / c4 run). usage: python scripts/experiments/build_exp.py tag[:DEF1,DEF2][:flag flag] ..."""
 import sys
 from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build libfa_gfx950.so from a source tree (e.g. a git archive of an older commit) for A/B runs.
-# usage: scripts/dev/build_lib_from.sh <src-root-with-include-and-csrc> <out.so>
+# usage: scripts/experiments/build_lib_from.sh <src-root-with-include-and-csrc> <out.so>
 set -e
 SRC=$1; OUT=$2; T=$(mktemp -d)
 CS=$SRC/flash_attention_cute_amd/csrc

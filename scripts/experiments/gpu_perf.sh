@@ -1,6 +1,6 @@
 #!/bin/bash
 # Quick perf loop on the GPU box: stamps diagnostic + SQ PMC pass + bench for the given configs.
-# usage: bash scripts/dev/gpu_perf.sh "c2 c4" [pmc-tag]
+# usage: bash scripts/experiments/gpu_perf.sh "c2 c4" [pmc-tag]
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out

@@ -23,7 +23,11 @@ for f in glob.glob(f"{src}/**/*counter_collection.csv", recursive=True):
         if any(k in r["Kernel_Name"] for k in KERNELS):
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
 mean = {k: sum(v) / len(v) for k, v in agg.items()}
-res = {"config": cfg, "source": note, "dispatches": {k: len(v) for k, v in agg.items()},
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from bench import lib_sha16  # noqa: E402  (the library these passes profiled: bench.py uses the
+#                                          traffic only while the loaded library has this hash)
+
+res = {"config": cfg, "source": note, "lib_sha16": lib_sha16(), "dispatches": {k: len(v) for k, v in agg.items()},
        "counters_mean_per_dispatch": mean}
 if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
     fetch = mean["FETCH_SIZE"] * 1024 * 2

@@ -43,7 +43,8 @@ def test_header_declares_the_boundary():
                                          "fa_fwd_gfx950_geometry", "fa_fwd_gfx950_ws",
                                          "fa_fwd_gfx950_workspace_size", "fa_fwd_gfx950_varlen",
                                          "fa_fwd_gfx950_varlen_check", "fa_fwd_gfx950_rope", "fa_rope_gfx950",
-                                         "fa_fwd_gfx950_window", "fa_fwd_gfx950_varlen_window"}
+                                         "fa_fwd_gfx950_window", "fa_fwd_gfx950_varlen_window", "fa_fwd_gfx950_padded",
+                                         "fa_fwd_gfx950_padded_workspace_size"}
 
 
 def test_every_declared_symbol_is_exported(lib):
@@ -83,7 +84,7 @@ def check(lib, p, dtype=0, causal=0):
 
 def test_abi_version(lib):
     lib.fa_abi_version.restype = ctypes.c_int
-    assert lib.fa_abi_version() == 5
+    assert lib.fa_abi_version() == 6
 
 
 def test_check_accepts_valid(lib):
@@ -276,3 +277,55 @@ def test_varlen_check(lib):
     assert lib.fa_fwd_gfx950_varlen_check(ctypes.byref(vp), 0, 1) == FA_ERR_UNSUPPORTED
     lib.fa_fwd_gfx950_varlen.restype = ctypes.c_int
     assert lib.fa_fwd_gfx950_varlen(ctypes.byref(vp), 0, 1, None) == FA_ERR_UNSUPPORTED  # validated, no launch
+
+
+def test_q_o_stride_bound_covers_the_interleaved_wave_slab(lib):
+    """fa_fwd_w4 addresses a wave's Q / O slab (block A + block B, 160 rows) with 32-bit offsets:
+    the q / o seqlen strides are bounded so that 160 rows fit, K / V by their 64-row tile."""
+    lim_qo = (0x7fffffff - 256) // (2 * 160) // 8 * 8   # largest multiple of 8 that fits
+    lim_kv = (0x7fffffff - 256) // (2 * 64) // 8 * 8
+    for t in "qo":
+        assert check(lib, good_params(**{f"{t}_seqlen_stride": lim_qo}))[0] == FA_OK
+        rc, err = check(lib, good_params(**{f"{t}_seqlen_stride": lim_qo + 8}))
+        assert rc == FA_ERR_UNSUPPORTED and "32-bit" in err
+    for t in "kv":
+        assert check(lib, good_params(**{f"{t}_seqlen_stride": lim_qo + 8}))[0] == FA_OK
+        assert check(lib, good_params(**{f"{t}_seqlen_stride": lim_kv + 8}))[0] == FA_ERR_UNSUPPORTED
+
+
+class FaPaddedParams(ctypes.Structure):
+    _fields_ = [("base", FaFwdParams), ("q_range", ctypes.c_void_p), ("k_range", ctypes.c_void_p)]
+
+
+def test_padded_struct_layout():
+    assert ctypes.sizeof(FaPaddedParams) == ctypes.sizeof(FaFwdParams) + 16
+
+
+def test_padded_entry_validates_before_touching_the_device(lib):
+    lib.fa_fwd_gfx950_padded.restype = ctypes.c_int
+    lib.fa_fwd_gfx950_padded.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
+                                         ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    lib.fa_fwd_gfx950_padded_workspace_size.restype = ctypes.c_int64
+    lib.fa_fwd_gfx950_padded_workspace_size.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64]
+    lib.fa_last_error.restype = ctypes.c_char_p
+    # decode shape with key ranges: the split-KV plan of the dense call
+    dec = FaPaddedParams(decode_params(b=1, sk=32768), None, 0x50000)
+    assert lib.fa_fwd_gfx950_padded_workspace_size(ctypes.byref(dec), 0, 0, -1) == ws_size(lib, dec.base)
+    # prefill shape with key ranges only: 2 * B int32 query ranges derived in the workspace
+    pre = FaPaddedParams(good_params(), None, 0x50000)
+    assert lib.fa_fwd_gfx950_padded_workspace_size(ctypes.byref(pre), 0, 1, -1) == 16
+    assert lib.fa_fwd_gfx950_padded_workspace_size(ctypes.byref(pre), 0, 1, 100) == 16  # window: prefill kernel
+    both = FaPaddedParams(good_params(), 0x60000, 0x50000)
+    assert lib.fa_fwd_gfx950_padded_workspace_size(ctypes.byref(both), 0, 1, -1) == 0
+    # ... and refuses to launch without that workspace
+    assert lib.fa_fwd_gfx950_padded(ctypes.byref(pre), 0, 1, -1, None, 0, None) == FA_ERR_INVALID_ARGUMENT
+    assert b"workspace" in lib.fa_last_error()
+    qonly = FaPaddedParams(good_params(), 0x60000, None)
+    assert lib.fa_fwd_gfx950_padded(ctypes.byref(qonly), 0, 1, -1, None, 0, None) == FA_ERR_INVALID_ARGUMENT
+    assert b"key ranges" in lib.fa_last_error()
+    odd = FaPaddedParams(good_params(), None, 0x50002)
+    assert lib.fa_fwd_gfx950_padded(ctypes.byref(odd), 0, 1, -1, None, 0, None) == FA_ERR_INVALID_ARGUMENT
+    bad = FaPaddedParams(good_params(headdim=136), None, 0x50000)
+    assert lib.fa_fwd_gfx950_padded(ctypes.byref(bad), 0, 1, -1, None, 0, None) == FA_ERR_UNSUPPORTED
+    assert lib.fa_fwd_gfx950_padded_workspace_size(ctypes.byref(bad), 0, 1, -1) == -1
+    assert lib.fa_fwd_gfx950_padded(None, 0, 1, -1, None, 0, None) == FA_ERR_INVALID_ARGUMENT
