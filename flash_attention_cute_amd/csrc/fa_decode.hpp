@@ -330,19 +330,22 @@ __global__ __launch_bounds__(256, 1) void fa_decode(const fa_fwd_params p, const
     }
 }
 
-// Merge n_split partials (O / l and lse = m*s' + log2 l, log2 units): one wave per (row block, row),
-// lane l owns d = 2l, 2l+1 (kD = 128) or d = l (kD = 64), so every partial row is one contiguous
-// 512 / 256-B wave read.
+// Merge n_split partials (O / l and lse = m*s' + log2 l, log2 units): one wave per valid (q-head,
+// position) row of a (batch, kv-head) -- a workgroup covers 4 of its a.rows rows, so the grid holds
+// only valid rows (B * Hkv * ceil(rows / 4) workgroups) -- lane l owns d = 2l, 2l+1 (kD = 128) or
+// d = l (kD = 64), so every partial row is one contiguous 512 / 256-B wave read.
 template <class DT, int kD, bool kExactD>
 __global__ __launch_bounds__(256) void fa_decode_combine(const fa_fwd_params p, const DecArgs a) {
     constexpr int DPL = kD / 64;  // d values per lane
-    const int wid = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int unit = wid / kDecRows, row = wid % kDecRows;
-    const int rb = unit % a.n_rb;
-    const int rg = rb * kDecRows + row;
-    if (unit >= (int)(p.batch_size * p.num_heads_kv) * a.n_rb || rg >= a.rows) return;
-    const int hkv = (unit / a.n_rb) % (int)p.num_heads_kv;
-    const int b = unit / (a.n_rb * (int)p.num_heads_kv);
+    const int lane = threadIdx.x & 63;
+    const int nb4 = (a.rows + 3) / 4;  // workgroups per (batch, kv-head)
+    const int bh = blockIdx.x / nb4;
+    const int rg = (blockIdx.x % nb4) * 4 + (threadIdx.x >> 6);  // row of the (batch, kv-head)
+    if (bh >= (int)(p.batch_size * p.num_heads_kv) || rg >= a.rows) return;
+    const int rb = rg / kDecRows, row = rg % kDecRows;
+    const int unit = bh * a.n_rb + rb;
+    const int hkv = bh % (int)p.num_heads_kv;
+    const int b = bh / (int)p.num_heads_kv;
     const int Sq = (int)p.seqlen_q, D = (int)p.headdim;
     const size_t base = (size_t)unit * a.n_split * kDecRows + row;
     float M = kNeg;
@@ -389,8 +392,9 @@ int launch_decode(const fa_fwd_params &p, DecArgs a, void *ws, hipStream_t strea
     }
     hipLaunchKernelGGL((fa_decode<DT, C, kD, kExact>), dim3((uint32_t)(units * a.n_split)), dim3(256), 0, stream, p, a);
     if (a.n_split > 1)
-        hipLaunchKernelGGL((fa_decode_combine<DT, kD, kExact>), dim3((uint32_t)(units * kDecRows / 4)), dim3(256), 0,
-                           stream, p, a);
+        hipLaunchKernelGGL((fa_decode_combine<DT, kD, kExact>),
+                           dim3((uint32_t)(p.batch_size * p.num_heads_kv * ((a.rows + 3) / 4))), dim3(256), 0, stream,
+                           p, a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "HIP launch failed: %s", hipGetErrorString(e));
     set_last_path(a.n_split > 1 ? kPathDecodeSplit : kPathDecode);

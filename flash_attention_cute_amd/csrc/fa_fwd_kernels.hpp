@@ -573,11 +573,14 @@ __global__ __launch_bounds__(kThreads) void fa_fwd_w8(const fa_fwd_params p, con
 #include "fa_agpr_asm.inc"
 
 // one MFMA a[BASE..BASE+15] += A.B into literal AGPRs (fa_agpr_asm.inc)
-template <bool kF16, int BASE>
+// (kW4: the form that also clobbers fa_fwd_w4's Q AGPRs a128..a191, fa_agpr_asm.inc)
+template <bool kF16, int BASE, bool kW4 = false>
 __device__ __forceinline__ void agpr_mfma(const u32x4 &a, const u32x4 &b) {
 #define FA_CASE(N)                                                    \
     if constexpr (BASE == N) {                                        \
-        if constexpr (kF16) fa_agpr_mfma_f16_##N(a, b);               \
+        if constexpr (kW4 && kF16) fa_agpr_mfma_w4_f16_##N(a, b);     \
+        else if constexpr (kW4) fa_agpr_mfma_w4_bf16_##N(a, b);       \
+        else if constexpr (kF16) fa_agpr_mfma_f16_##N(a, b);          \
         else fa_agpr_mfma_bf16_##N(a, b);                             \
     }
     FA_CASE(0) FA_CASE(16) FA_CASE(32) FA_CASE(48) FA_CASE(64) FA_CASE(80) FA_CASE(96) FA_CASE(112)
@@ -1342,7 +1345,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             // one counted wait per 16-key step: its V^T fragments were read in the first DTL gaps
             // of the previous step, two per gap
             if constexpr (kk > 0 && i == 0) __builtin_amdgcn_s_waitcnt(kLgkm0);
-            if constexpr (!(pdead && X == 0)) agpr_mfma<F, X * 16 * DTL + 16 * dt>(va[kk & 1][dt], P[cp][4 * X + kk]);
+            if constexpr (!(pdead && X == 0)) agpr_mfma<F, X * 16 * DTL + 16 * dt, true>(va[kk & 1][dt], P[cp][4 * X + kk]);
             FA_SCHED_FENCE();  // (see phase 1)
             if constexpr (kk + 1 < 4 && i < DTL) {
                 rd(kk + 1, 2 * i, va[(kk + 1) & 1]);
@@ -1461,16 +1464,20 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // ---- pipelined tiles: iteration j = P1(S_j || softmax half 2 of j-1, DMA K_{j+1}, V_j),
     //      P2(O += P_{j-1} V_{j-1} || softmax half 1 of j), rescale, barrier -------------------
     // causal diagonal / Sk tail: scores of keys past a row's last visible key -> kNeg
-    auto mask = [&](f32x16 &s0, f32x16 &s1, const int row, const int key0) __attribute__((always_inline)) {
-        const int lim = kCausal ? min(Sk - 1, row + diag) : Sk - 1;
+    // row0: the block's first query row (wave-uniform; the lane's row is row0 + r). Score i of half
+    // hf is key key0 + 32 hf + c_i + 4 h with c_i = (i & 3) + 8 (i >> 2): against the lane's last
+    // visible key minus key0 + 4 h, each score is one compare with an inline constant and a select.
+    auto mask = [&](f32x16 &s0, f32x16 &s1, const int row0, const int key0) __attribute__((always_inline)) {
         if (wl < 0) {
+            const int e = (kCausal ? min(Sk - 1, row0 + r + diag) : Sk - 1) - key0 - 4 * h;
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                const int kk = key0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                if (kk > lim) s0[i] = kNeg;
-                if (kk + 32 > lim) s1[i] = kNeg;
+                if ((i & 3) + 8 * (i >> 2) > e) s0[i] = kNeg;
+                if ((i & 3) + 8 * (i >> 2) + 32 > e) s1[i] = kNeg;
             }
         } else {  // and keys left of the row's window
+            const int row = row0 + r;
+            const int lim = kCausal ? min(Sk - 1, row + diag) : Sk - 1;
             const int lo = row + diag - wl;
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
@@ -1507,10 +1514,10 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         if constexpr (mk != 0) {  // diagonal / tail tile: mask S before phase 2
             if constexpr (mk == 1) {
                 s_ready(S[c][0], S[c][1]);
-                mask(S[c][0], S[c][1], mw + r, j * kBlockN);
+                mask(S[c][0], S[c][1], mw, j * kBlockN);
             }
             s_ready(S[c][2], S[c][3]);
-            mask(S[c][2], S[c][3], mw + kRowB + r, j * kBlockN);
+            mask(S[c][2], S[c][3], mw + kRowB, j * kBlockN);
         }
         FA_STAMP(sb);
 #if defined(FA_EXP_NOSM)
@@ -1599,8 +1606,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         phase1(K, IC<0>{}, IC<0>{}, IC<0>{}, k_rsrc(j), k_rsrc(j), IC<0>{});
         s_ready(S[0][0], S[0][1]);
         s_ready(S[0][2], S[0][3]);
-        mask(S[0][0], S[0][1], mw + r, key0);
-        mask(S[0][2], S[0][3], mw + kRowB + r, key0);
+        mask(S[0][0], S[0][1], mw, key0);
+        mask(S[0][2], S[0][3], mw + kRowB, key0);
         sm1_all(IC<0>{});
         rescale(j == j_lo);
         sm2_all(IC<0>{}, IC<0>{});

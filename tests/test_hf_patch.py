@@ -48,8 +48,19 @@ class patched:
         self.cls.forward = self.orig
 
 
-def run_layer(attn_cls, cfg, dev, dtype, seqs=(7, 1, 1), patch=False, seed=0):
-    """Prefill seqs[0] tokens, then decode the rest one step at a time, through a DynamicCache."""
+def bottom_right_mask4(b, s, pos, dev):
+    """[B, 1, s, pos + s] bool (True = attend): s new tokens at positions pos.. see every key up to
+    their own position -- the kernel's bottom-right causal alignment (reference csrc/mask.cuh:37-39)
+    written as the explicit mask an unpatched HF layer honours."""
+    p_ = torch.arange(pos, pos + s, device=dev)[:, None]
+    n = torch.arange(pos + s, device=dev)[None, :]
+    return (n <= p_)[None, None].expand(b, 1, s, pos + s)
+
+
+def run_layer(attn_cls, cfg, dev, dtype, seqs=(7, 1, 1), patch=False, seed=0, explicit_mask=False):
+    """Prefill seqs[0] tokens, then decode the rest one step at a time, through a DynamicCache.
+    explicit_mask: pass the bottom-right causal mask of every step (unpatched reference runs of steps
+    with Sq < Sk, where HF's mask-free SDPA call would be top-left causal)."""
     torch.manual_seed(seed)
     layer = attn_cls(cfg, layer_idx=0).to(dev, dtype).eval()
     rope = (ml.LlamaRotaryEmbedding if attn_cls is ml.LlamaAttention else mq.Qwen2RotaryEmbedding)(cfg).to(dev)
@@ -65,7 +76,8 @@ def run_layer(attn_cls, cfg, dev, dtype, seqs=(7, 1, 1), patch=False, seed=0):
             pid = torch.arange(pos, pos + s, device=dev)[None].expand(2, -1)
             pe = rope(x, pid)
             # unpatched HF builds no mask for SDPA here; pass is_causal through the module
-            o, _ = layer(x[:, pos:pos + s], position_embeddings=pe, attention_mask=None, past_key_values=cache,
+            mask = bottom_right_mask4(2, s, pos, dev) if explicit_mask else None
+            o, _ = layer(x[:, pos:pos + s], position_embeddings=pe, attention_mask=mask, past_key_values=cache,
                          cache_position=pid[0])
             outs.append(o)
             if patch and torch.device(dev).type == "cuda":
@@ -249,31 +261,119 @@ def test_patch_gqa_layer_matches_hf_on_gpu(device, attn_cls, mk, dtype):
     from flash_attention_cute_amd import _debug
 
     _debug.set_knobs()  # product defaults
-    ref = run_layer(attn_cls, cfg, device, torch.float32, seqs=seqs, patch=False)
+    # the reference: unpatched transformers in fp32 with the bottom-right causal mask written out, so
+    # the Sq < Sk chunk is compared too (mask-free SDPA would be top-left causal there)
+    ref = run_layer(attn_cls, cfg, device, torch.float32, seqs=seqs, patch=False, explicit_mask=True)
     got = run_layer(attn_cls, cfg, device, dtype, seqs=seqs, patch=True)
     # prefill on the pipelined w4 kernel; the Sq == 1 steps on the decode kernel; the 37-row chunk
     # (4 q-heads x 37 rows > 64) on w4
     assert run_layer.paths[0] == "w4" and run_layer.paths[3] == "w4", run_layer.paths
     assert all(p_ in ("decode", "decode_split") for p_ in run_layer.paths[1:3]), run_layer.paths
-    # the last chunk (Sq < Sk): unpatched HF SDPA with attention_mask=None uses is_causal only when
-    # q_len > 1 and Sq == Sk; compare prefill + decode rows, and the chunk against a bottom-right ref
     tol = 2e-2 if dtype == torch.bfloat16 else 4e-3
-    n = seqs[0] + seqs[1] + seqs[2]
-    torch.testing.assert_close(got[:, :n].float(), ref[:, :n], atol=tol, rtol=0)
+    assert got.shape[1] == sum(seqs)
+    torch.testing.assert_close(got.float(), ref, atol=tol, rtol=0)  # every row, the chunk included
+
+
+def greedy_margins(model, seq, n_prompt, mask):
+    """Top-1 minus top-2 logit (fp32 model) at every generated position of ``seq``: how far each greedy
+    choice is from a tie."""
+    full = torch.cat([mask, torch.ones_like(seq[:, n_prompt:])], dim=1)
+    pid = (full.long().cumsum(1) - 1).clamp(min=0)
+    with torch.no_grad():
+        logits = model(seq, attention_mask=full, position_ids=pid).logits.float()[:, n_prompt - 1:-1]
+    top2 = logits.topk(2, dim=-1).values
+    return (top2[..., 0] - top2[..., 1])
+
+
+def tiny_generator(device, padded):
+    """A 2-layer GQA Llama (Hq 8, Hkv 2, D 128; seeded random weights, initializer_range 0.3 so the
+    logits spread over several units) and a 48-token prompt batch of 2 (row 1 left-padded by 17),
+    generated on ``device``."""
+    cfg = tiny_llama(hq=8, hkv=2, d=128, layers=2)
+    cfg.initializer_range = 0.3
+    # seed 8: on MI355X the fp32 greedy trajectory's top-2 margins are >= 0.15 for both prompts and
+    # unpatched fp16 reproduces it (scripts/experiments/gen_seed_search.py, profiles/r3_gen_seed.log)
+    torch.manual_seed(8)
+    model = transformers.LlamaForCausalLM(cfg).to(device).eval()
+    ids = torch.randint(0, cfg.vocab_size, (2, 48), device=device)
+    mask = torch.ones_like(ids)
+    if padded:
+        mask[1, :17] = 0
+        ids[1, :17] = 0
+    return model, ids, mask
 
 
 @pytest.mark.gpu
-def test_patched_llama_model_generates_same_tokens_as_hf(device):
-    cfg = tiny_llama(hq=8, hkv=2, d=128, layers=2)
-    torch.manual_seed(0)
-    model = transformers.LlamaForCausalLM(cfg).to(device, torch.bfloat16).eval()
-    ids = torch.randint(0, cfg.vocab_size, (2, 64), device=device)
+@pytest.mark.parametrize("padded", [False, True], ids=["dense", "left_padded"])
+def test_patched_llama_greedy_generate_matches_hf_fp16(device, padded):
+    """Greedy ``generate`` of 24 tokens through a DynamicCache in fp16 (prefill + 23 decode steps on the
+    split-KV kernel; with left padding, the padded path in place): the patched model produces exactly
+    the token ids of unpatched transformers (SDPA) in fp16 and of the fp32 model. Premise, checked: the
+    fp32 greedy trajectory has a top-2 logit margin >= 0.1 at every step, far above fp16 error."""
+    from flash_attention_cute_amd import _debug
+
+    _debug.set_knobs()
+    model, ids, mask = tiny_generator(device, padded)
+    kw = dict(attention_mask=mask, max_new_tokens=24, do_sample=False, pad_token_id=0)
     with torch.no_grad():
-        ref = model(ids).logits.float()
+        ref32 = model.generate(ids, **kw)
+    margins = greedy_margins(model, ref32, ids.shape[1], mask)
+    assert margins.min().item() >= 0.1, margins.min().item()  # the premise
+    model = model.half()
+    with torch.no_grad():
+        ref = model.generate(ids, **kw)
         with patched(ml.LlamaAttention):
-            got = model(ids).logits.float()
-    assert (got - ref).abs().max().item() < 5e-2
-    assert (got.argmax(-1) == ref.argmax(-1)).float().mean().item() > 0.95
+            got = model.generate(ids, **kw)
+    assert got.shape == (2, 48 + 24)
+    assert torch.equal(got, ref), (got[:, 48:], ref[:, 48:])
+    assert torch.equal(got, ref32), (got[:, 48:], ref32[:, 48:])
+
+
+def teacher_forced_decode(model, seq, mask, n_prompt, patch):
+    """Logits of every generated position of ``seq``: prefill of the prompt, then one decode step per
+    token of ``seq`` through a DynamicCache (the decode path), fp32 copies."""
+    full = torch.cat([mask, torch.ones_like(seq[:, n_prompt:])], dim=1)
+    pid = (full.long().cumsum(1) - 1).clamp(min=0)
+    cache = DynamicCache()
+    outs = []
+    with torch.no_grad(), warnings.catch_warnings(), (patched(ml.LlamaAttention) if patch else _null()):
+        warnings.simplefilter("ignore")
+        o = model(seq[:, :n_prompt], attention_mask=full[:, :n_prompt], position_ids=pid[:, :n_prompt],
+                  past_key_values=cache, use_cache=True)
+        outs.append(o.logits[:, -1].float())
+        for t in range(n_prompt, seq.shape[1] - 1):
+            o = model(seq[:, t:t + 1], attention_mask=full[:, :t + 1], position_ids=pid[:, t:t + 1],
+                      past_key_values=cache, use_cache=True)
+            outs.append(o.logits[:, -1].float())
+    return torch.stack(outs, 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("padded", [False, True], ids=["dense", "left_padded"])
+def test_patched_llama_decode_logits_bf16_bar(device, padded):
+    """bf16: greedy token ids are not a stable bar here (unpatched HF bf16 itself departs from the fp32
+    trajectory), so the bar is BASELINE.md's: teacher-forced along the fp32 greedy trajectory (prefill,
+    then 23 single-token decode steps through a DynamicCache -- the split-KV kernel, padded path with
+    left padding), the patched model's logits stay within 2x the error of unpatched transformers bf16
+    against fp32 (max and mean), and its greedy choice agrees with fp32 at least as often."""
+    from flash_attention_cute_amd import _debug
+
+    _debug.set_knobs()
+    model, ids, mask = tiny_generator(device, padded)
+    with torch.no_grad():
+        seq = model.generate(ids, attention_mask=mask, max_new_tokens=24, do_sample=False, pad_token_id=0)
+    l32 = teacher_forced_decode(model, seq, mask, 48, patch=False)
+    model = model.to(torch.bfloat16)
+    lhf = teacher_forced_decode(model, seq, mask, 48, patch=False)
+    lgot = teacher_forced_decode(model, seq, mask, 48, patch=True)
+    assert _debug.last_path() in ("decode", "decode_split"), _debug.last_path()
+    e_hf, e_got = (lhf - l32).abs(), (lgot - l32).abs()
+    assert e_got.max().item() <= 2 * e_hf.max().item(), (e_got.max().item(), e_hf.max().item())
+    assert e_got.mean().item() <= 2 * e_hf.mean().item(), (e_got.mean().item(), e_hf.mean().item())
+    tok32 = l32.argmax(-1)
+    agree_got = (lgot.argmax(-1) == tok32).float().mean().item()
+    agree_hf = (lhf.argmax(-1) == tok32).float().mean().item()
+    assert agree_got >= agree_hf - 0.05, (agree_got, agree_hf)
 
 
 @pytest.mark.gpu
