@@ -98,7 +98,11 @@ __global__ __launch_bounds__(256, 1) void fa_decode(const fa_fwd_params p, const
 
     // ---- this wave's tiles: a contiguous quarter of the split --------------------------------
     const int n_tiles = (Sk + kDecKeys - 1) / kDecKeys;
-    const int s_lo = min(split * a.tps, n_tiles), s_hi = min(s_lo + a.tps, n_tiles);
+    // splits of the plan's (maximum) length; with per-sequence key ranges every split takes an equal
+    // share of THIS sequence's tiles instead, so a short sequence leaves no split empty and a long
+    // one no split overfull
+    const int tps = a.k_rng ? (n_tiles + a.n_split - 1) / a.n_split : a.tps;
+    const int s_lo = min(split * tps, n_tiles), s_hi = min(s_lo + tps, n_tiles);
     const int per_wave = (s_hi - s_lo + kDecWaves - 1) / kDecWaves;
     const int t_lo = min(s_lo + wave * per_wave, s_hi), t_hi = min(t_lo + per_wave, s_hi);
 

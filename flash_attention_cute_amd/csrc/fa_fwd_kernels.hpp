@@ -689,6 +689,27 @@ __device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 7\n\ts_nop 7\
 // s_waitcnt lgkmcnt(0) alone (gfx9 encoding: vmcnt 63, expcnt 7, lgkmcnt 0)
 constexpr int kLgkm0 = 0xC07F;
 
+// Causal / tail mask of score I of both key halves of a block (fa_fwd_w4 `mask`): key offsets
+// c = (I & 3) + 8 (I >> 2) and c + 32 against e (the lane's last visible key minus key0 + 4h);
+// hidden scores become kNeg. Two independent compare -> select chains (VCC and an SGPR pair).
+// (neg: kNeg in a VGPR -- gfx9 VOP3 reads one SGPR / literal at most, and the select's mask is one)
+template <int I>
+__device__ __forceinline__ void mask_pair(f32x16 &s0, f32x16 &s1, const int e, const float neg) {
+    constexpr int c = (I & 3) + 8 * (I >> 2);
+    float x0 = s0[I], x1 = s1[I];
+    uint64_t m;
+    asm volatile(
+        "v_cmp_le_i32_e32 vcc, %4, %3\n\t"
+        "v_cmp_le_i32_e64 %2, %5, %3\n\t"
+        "v_cndmask_b32_e64 %0, %6, %0, vcc\n\t"
+        "v_cndmask_b32_e64 %1, %6, %1, %2"
+        : "+v"(x0), "+v"(x1), "=&s"(m)
+        : "v"(e), "n"(c), "n"(c + 32), "v"(neg)
+        : "vcc");
+    s0[I] = x0;
+    s1[I] = x1;
+}
+
 // Opaque redefinition: ties a value to this point of the (volatile-asm ordered) instruction stream,
 // so IR-level sinking / hoisting cannot move the VALU slices out of their MFMA gap.
 #ifndef FA_NOPIN
@@ -1467,14 +1488,15 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // row0: the block's first query row (wave-uniform; the lane's row is row0 + r). Score i of half
     // hf is key key0 + 32 hf + c_i + 4 h with c_i = (i & 3) + 8 (i >> 2): against the lane's last
     // visible key minus key0 + 4 h, each score is one compare with an inline constant and a select.
+    // (inline asm: two independent compare -> select chains per score pair, one through VCC and one
+    // through an SGPR pair, so no select waits on the compare just before it; compiled C++ turned
+    // the same selects into SALU-mask chains that cost ~1.9k cycles per masked tile, stamps r3)
     auto mask = [&](f32x16 &s0, f32x16 &s1, const int row0, const int key0) __attribute__((always_inline)) {
         if (wl < 0) {
             const int e = (kCausal ? min(Sk - 1, row0 + r + diag) : Sk - 1) - key0 - 4 * h;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                if ((i & 3) + 8 * (i >> 2) > e) s0[i] = kNeg;
-                if ((i & 3) + 8 * (i >> 2) + 32 > e) s1[i] = kNeg;
-            }
+            float neg = kNeg;
+            asm volatile("" : "+v"(neg));  // (materialised once, in a VGPR)
+            static_for<16>([&](auto I) { mask_pair<decltype(I)::value>(s0, s1, e, neg); });
         } else {  // and keys left of the row's window
             const int row = row0 + r;
             const int lim = kCausal ? min(Sk - 1, row + diag) : Sk - 1;
@@ -1511,6 +1533,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #else
         phase1(lds + KV0 + c * T, PAR, IC<1>{}, IC<1>{}, kr, vr, AD{});
 #endif
+#ifndef FA_EXP_NOMASK  // (timing experiment of the stamps build only: no mask step, wrong results)
         if constexpr (mk != 0) {  // diagonal / tail tile: mask S before phase 2
             if constexpr (mk == 1) {
                 s_ready(S[c][0], S[c][1]);
@@ -1519,6 +1542,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             s_ready(S[c][2], S[c][3]);
             mask(S[c][2], S[c][3], mw + kRowB, j * kBlockN);
         }
+#endif
         FA_STAMP(sb);
 #if defined(FA_EXP_NOSM)
         phase2(lds + KV0 + (2 + pr) * T, IC<pr>{}, PAR, IC<0>{}, AD{});
@@ -1532,11 +1556,16 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         __syncthreads();
 #ifdef FA_STAMPS
         const unsigned long long se = __builtin_amdgcn_s_memtime();
-        st_acc[0] += sb - sa;
-        st_acc[1] += sc_ - sb;
-        st_acc[2] += sd - sc_;
-        st_acc[3] += se - sd;
-        st_acc[4] += 1;
+#ifdef FA_STAMPS_MASKED  // (diagnostic: the tile columns of the record count masked tiles only)
+        if constexpr (mk != 0)
+#endif
+        {
+            st_acc[0] += sb - sa;
+            st_acc[1] += sc_ - sb;
+            st_acc[2] += sd - sc_;
+            st_acc[3] += se - sd;
+            st_acc[4] += 1;
+        }
 #endif
     };
     // every tile runs pipelined: first the tiles without a masked score, then (a second loop, so

@@ -67,6 +67,7 @@ assert lib.fa_fwd_gfx950(ctypes.byref(p), 0 if dt == torch.float16 else 1, int(c
 torch.cuda.synchronize()
 lib.fa_debug_set_stamps(ctypes.c_void_p(0))
 s = buf.view(-1, 12).cpu().double()
+s = s[s[:, 0] > 0]  # records of Q blocks that ran (an empty q-tile block writes none)
 names = ["total", "p1", "p2+resc", "dma_wait", "barrier", "tiles", "drain", "prologue", "epilogue", "realtime"]
 med = s.median(dim=0).values
 print(f"{cfg['workload']} [{variant}]: {n} warm launches, {s.shape[0]} waves")
@@ -80,6 +81,16 @@ print(f"  in-kernel clock median {float(clk.median()):.3f} GHz")
 start = s[:, 10] - s[:, 10].min()
 print(f"  launch span {float((s[:, 10] + s[:, 0]).max() - s[:, 10].min()):.0f} cycles, start spread "
       f"{float(start.max()):.0f}")
+# whole-launch accounting (wave 0 of each Q block): busy share of the launch span over the grid's
+# workgroups (end-of-launch imbalance), and the share of the block switch in the busy cycles
+w0 = s[torch.arange(s.shape[0]) % WAVES == 0]
+span = float((w0[:, 10] + w0[:, 0]).max() - w0[:, 10].min())
+grid = min(nwg, 256)
+busy = float(w0[:, 0].sum())
+switch = float((w0[:, 6] + w0[:, 7] + w0[:, 8]).sum())
+loop = float((w0[:, 1] + w0[:, 2] + w0[:, 3] + w0[:, 4]).sum())
+print(f"  utilisation (busy / (span x {grid} workgroups)) {busy / (span * grid):.3f}; of the busy cycles: "
+      f"tiles {loop / busy:.3f}, switch (drain + prologue + epilogue) {switch / busy:.3f}")
 for i, nm in [(6, "drain"), (7, "prologue"), (8, "epilogue")]:
     qs = torch.quantile(s[:, i], torch.tensor([0.1, 0.5, 0.9, 0.99], dtype=torch.float64))
     print(f"  {nm:10s} p10 {qs[0]:8.0f}  p50 {qs[1]:8.0f}  p90 {qs[2]:8.0f}  p99 {qs[3]:8.0f}")
