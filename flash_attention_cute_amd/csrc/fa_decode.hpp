@@ -81,12 +81,12 @@ __global__ __launch_bounds__(256, 1) void fa_decode(const fa_fwd_params p, const
     const int Sq = (int)p.seqlen_q, D = (int)p.headdim;  // Sq: positions per q-head (row addressing)
     const float sc = p.softmax_scale;
     const float thr_raw = kRescaleThr / sc;
-    // this batch row's keys: absolute rows [k0, k0 + Sk) of k / v (a padded batch's key range,
-    // DecArgs, whose k / v batch strides the host zeroes); else every key
+    // this batch row's keys: positions [k0, k0 + Sk) (a padded batch's key range, DecArgs); else
+    // every key
     int k0 = 0, Sk = (int)p.seqlen_kv;
-    if (a.k_rng) {
-        k0 = a.k_rng[b];
-        Sk = max(a.k_rng[b + a.rng_hi] - k0, 0);
+    if (a.k_lo) {
+        k0 = a.k_lo[b];
+        Sk = max(a.k_hi[b] - k0, 0);
     }
     const int diag = Sk - Sq;
 
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256, 1) void fa_decode(const fa_fwd_params p, const
     // splits of the plan's (maximum) length; with per-sequence key ranges every split takes an equal
     // share of THIS sequence's tiles instead, so a short sequence leaves no split empty and a long
     // one no split overfull
-    const int tps = a.k_rng ? (n_tiles + a.n_split - 1) / a.n_split : a.tps;
+    const int tps = a.k_lo ? (n_tiles + a.n_split - 1) / a.n_split : a.tps;
     const int s_lo = min(split * tps, n_tiles), s_hi = min(s_lo + tps, n_tiles);
     const int per_wave = (s_hi - s_lo + kDecWaves - 1) / kDecWaves;
     const int t_lo = min(s_lo + wave * per_wave, s_hi), t_hi = min(t_lo + per_wave, s_hi);

@@ -110,7 +110,7 @@ using fa::launch_one;
 
 bool aligned16(const void *ptr) { return ((uintptr_t)ptr & 15) == 0; }
 
-constexpr fa::PathArgs kNoPath{nullptr, nullptr, 0, 0, -1, 0, nullptr, nullptr};
+constexpr fa::PathArgs kNoPath{nullptr, nullptr, 0, 0, -1, 0, nullptr, nullptr, nullptr, nullptr};
 
 int check_params(const fa_fwd_params *p, int dtype, int causal) {
     (void)causal;
@@ -195,8 +195,8 @@ int dispatch(const fa_fwd_params *params, int dtype, int causal, void *ws, int64
     const fa_fwd_params &p = *params;
     if (use_decode(p, ranges)) {
         fa::DecArgs a = fa::decode_plan(p, ws ? fa::kDecMaxSplit : 1);
-        a.rng_hi = ranges.rng_hi;
-        a.k_rng = ranges.k_rng;
+        a.k_lo = ranges.k_lo;
+        a.k_hi = ranges.k_hi;
         if (ws && fa::decode_ws_bytes(p, a) > ws_bytes)
             return set_err(FA_ERR_INVALID_ARGUMENT, "workspace of %lld bytes is smaller than the %lld required",
                            (long long)ws_bytes, (long long)fa::decode_ws_bytes(p, a));
@@ -235,7 +235,7 @@ int dispatch_varlen(const fa_varlen_params *v, int dtype, int causal, void *stre
     // packed rows: sequence b is rows [cu[b], cu[b + 1]) of the tensors, no batch offset
     fa_fwd_params p = v->base;
     p.q_batch_stride = p.k_batch_stride = p.v_batch_stride = p.o_batch_stride = 0;
-    const fa::PathArgs xa{nullptr, nullptr, 0, 0, window_left < 0 ? -1 : (int)window_left, 1, cq, ck};
+    const fa::PathArgs xa{nullptr, nullptr, 0, 0, window_left < 0 ? -1 : (int)window_left, 1, cq, ck, nullptr, nullptr};
     if (dtype == FA_DTYPE_F16)
         return causal ? launch<fa::F16, true>(p, s, xa) : launch<fa::F16, false>(p, s, xa);
     return causal ? launch<fa::BF16, true>(p, s, xa) : launch<fa::BF16, false>(p, s, xa);
@@ -243,35 +243,40 @@ int dispatch_varlen(const fa_varlen_params *v, int dtype, int causal, void *stre
 
 int check_padded(const fa_padded_params *v, int dtype, int causal) {
     if (!v) return set_err(FA_ERR_INVALID_ARGUMENT, "params is NULL");
-    if (v->q_range && !v->k_range)
-        return set_err(FA_ERR_INVALID_ARGUMENT, "query ranges need key ranges (pass k starts 0, ends Sk)");
-    if (((uintptr_t)v->q_range & 3) || ((uintptr_t)v->k_range & 3))
-        return set_err(FA_ERR_INVALID_ARGUMENT, "ranges must be 4-byte aligned int32 arrays");
+    if (!v->k_start != !v->k_end || !v->q_start != !v->q_end)
+        return set_err(FA_ERR_INVALID_ARGUMENT, "k_start / k_end (and q_start / q_end) must be given together");
+    const int32_t *arr[4] = {v->q_start, v->q_end, v->k_start, v->k_end};
+    for (int i = 0; i < 4; ++i)
+        if ((uintptr_t)arr[i] & 3) return set_err(FA_ERR_INVALID_ARGUMENT, "ranges must be 4-byte aligned int32 arrays");
     if (v->base.batch_size > 0x7fffffffLL) return set_err(FA_ERR_UNSUPPORTED, "batch too large");
     return check_params(&v->base, dtype, causal);
 }
 
-// Padded batches: per-sequence query / key ranges inside dense tensors. Few rows per kv-head run
-// the split-KV decode kernel (the ranges bound each sequence's key stream), everything else
-// fa_fwd_w4; window_left >= 0 applies the local window per sequence (prefill kernel only).
-// the prefill kernel takes key ranges only together with query ranges: "every query row" of batch
-// row b as absolute rows [b * rows_per_batch, b * rows_per_batch + Sq) (fa_fwd_w4 reads both)
-__global__ void fill_all_rows(int32_t *rng, int batch, int64_t rows_per_batch, int sq) {
+// The decode kernel reads per-sequence key positions as given. The prefill kernel addresses a
+// ranged sequence by ABSOLUTE rows (row r at base + r * seqlen stride, batch strides unused), so the
+// dispatcher converts the positions into [2, B] row arrays in the workspace: rows of batch row b =
+// b * rows_per_batch + position (a missing range is the whole dimension).
+__global__ void padded_rows(int32_t *q_rng, int32_t *k_rng, const int32_t *qs, const int32_t *qe, const int32_t *ks,
+                            const int32_t *ke, int batch, int64_t q_rpb, int64_t k_rpb, int sq, int sk) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b < batch) {
-        rng[b] = (int32_t)(b * rows_per_batch);
-        rng[batch + b] = (int32_t)(b * rows_per_batch + sq);
+        q_rng[b] = (int32_t)(b * q_rpb + (qs ? qs[b] : 0));
+        q_rng[batch + b] = (int32_t)(b * q_rpb + (qe ? qe[b] : sq));
+        k_rng[b] = (int32_t)(b * k_rpb + (ks ? ks[b] : 0));
+        k_rng[batch + b] = (int32_t)(b * k_rpb + (ke ? ke[b] : sk));
     }
 }
 
-// a padded launch that the prefill kernel serves with key ranges but no query ranges derives the
-// query ranges into the workspace: bytes it needs there (0 if none)
-int64_t padded_qfill_bytes(const fa_padded_params *v, int64_t window_left) {
-    if (!v->k_range || v->q_range) return 0;
-    if (window_left < 0 && use_decode(v->base)) return 0;  // the decode kernel takes key ranges alone
-    return (2 * v->base.batch_size * 4 + 15) / 16 * 16;
+bool padded_on_decode(const fa_padded_params *v, int64_t window_left) {
+    return !v->q_start && window_left < 0 && use_decode(v->base);
 }
+// workspace of a prefill-kernel padded launch: the two [2, B] row arrays, 16-B aligned
+int64_t padded_rows_bytes(const fa_padded_params *v) { return (4 * v->base.batch_size * 4 + 15) / 16 * 16; }
 
+// Padded batches: per-sequence query / key positions inside dense tensors. Few rows per kv-head (no
+// query ranges, no window) run the split-KV decode kernel on each sequence's key positions, all else
+// fa_fwd_w4 on the row arrays built in the workspace; window_left >= 0 applies the local window per
+// sequence.
 int dispatch_padded(const fa_padded_params *v, int dtype, int causal, int64_t window_left, void *ws,
                     int64_t ws_bytes, void *stream) {
     g_last_path = fa::kPathNone;
@@ -279,31 +284,40 @@ int dispatch_padded(const fa_padded_params *v, int dtype, int causal, int64_t wi
     if (rc != FA_OK) return rc;
     if (window_left > 0x3fffffffLL) window_left = 0x3fffffff;
     hipStream_t s = (hipStream_t)stream;
-    // ranges hold absolute rows: the batch strides of ranged tensors are not used
-    fa_fwd_params p = v->base;
-    const int32_t *q_range = v->q_range;
-    const int64_t qfill = padded_qfill_bytes(v, window_left);
-    if (qfill > 0) {
-        const fa_fwd_params &b = v->base;
-        if (b.q_seqlen_stride <= 0 || b.q_batch_stride % b.q_seqlen_stride != 0 ||
-            b.o_batch_stride * b.q_seqlen_stride != b.q_batch_stride * b.o_seqlen_stride ||
-            (b.batch_size - 1) * (b.q_batch_stride / b.q_seqlen_stride) + b.seqlen_q > 0x7fffffffLL)
-            return set_err(FA_ERR_INVALID_ARGUMENT,
-                           "without q_range, q and o need batch strides that are equal multiples of their seqlen "
-                           "strides (or pass q_range)");
-        if (!ws || ws_bytes < qfill)
-            return set_err(FA_ERR_INVALID_ARGUMENT, "workspace of %lld bytes is smaller than the %lld required",
-                           (long long)ws_bytes, (long long)qfill);
-        int32_t *qr = (int32_t *)ws;
-        hipLaunchKernelGGL(fill_all_rows, dim3((uint32_t)((b.batch_size + 255) / 256)), dim3(256), 0, s, qr,
-                           (int)b.batch_size, b.q_batch_stride / b.q_seqlen_stride, (int)b.seqlen_q);
-        q_range = qr;
+    if (padded_on_decode(v, window_left)) {
+        fa::PathArgs xa = kNoPath;
+        xa.k_lo = v->k_start;
+        xa.k_hi = v->k_end;
+        return dispatch(&v->base, dtype, causal, ws, ws_bytes, stream, xa);
     }
-    if (v->k_range) p.k_batch_stride = p.v_batch_stride = 0;
-    if (q_range) p.q_batch_stride = p.o_batch_stride = 0;
-    const fa::PathArgs xa{nullptr, nullptr, 0, 0, window_left < 0 ? -1 : (int)window_left, (int)p.batch_size,
-                          q_range, v->k_range};
-    if (window_left < 0) return dispatch(&p, dtype, causal, ws, ws_bytes, stream, xa);
+    const fa_fwd_params &b = v->base;
+    auto rpb = [](int64_t bstride, int64_t sstride, int64_t nb) -> int64_t {
+        if (nb == 1) return 0;
+        return (sstride > 0 && bstride % sstride == 0) ? bstride / sstride : -1;
+    };
+    const int64_t q_rpb = rpb(b.q_batch_stride, b.q_seqlen_stride, b.batch_size);
+    const int64_t k_rpb = rpb(b.k_batch_stride, b.k_seqlen_stride, b.batch_size);
+    if (q_rpb < 0 || k_rpb < 0 || rpb(b.o_batch_stride, b.o_seqlen_stride, b.batch_size) != q_rpb ||
+        rpb(b.v_batch_stride, b.v_seqlen_stride, b.batch_size) != k_rpb ||
+        (b.batch_size - 1) * q_rpb + b.seqlen_q > 0x7fffffffLL || (b.batch_size - 1) * k_rpb + b.seqlen_kv > 0x7fffffffLL)
+        return set_err(FA_ERR_INVALID_ARGUMENT,
+                       "padded prefill: the batch strides of q / o (k / v) must be the same multiple of their seqlen "
+                       "strides");
+    const int64_t need = padded_rows_bytes(v);
+    if (!ws || ws_bytes < need)
+        return set_err(FA_ERR_INVALID_ARGUMENT, "workspace of %lld bytes is smaller than the %lld required",
+                       (long long)ws_bytes, (long long)need);
+    int32_t *q_rng = (int32_t *)ws, *k_rng = q_rng + 2 * b.batch_size;
+    hipLaunchKernelGGL(padded_rows, dim3((uint32_t)((b.batch_size + 255) / 256)), dim3(256), 0, s, q_rng, k_rng,
+                       v->q_start, v->q_end, v->k_start, v->k_end, (int)b.batch_size, q_rpb, k_rpb, (int)b.seqlen_q,
+                       (int)b.seqlen_kv);
+    fa_fwd_params p = b;
+    p.q_batch_stride = p.k_batch_stride = p.v_batch_stride = p.o_batch_stride = 0;
+    fa::PathArgs xa = kNoPath;
+    xa.window_left = window_left < 0 ? -1 : (int)window_left;
+    xa.rng_hi = (int)b.batch_size;
+    xa.q_rng = q_rng;
+    xa.k_rng = k_rng;
     if (dtype == FA_DTYPE_F16)
         return causal ? launch<fa::F16, true>(p, s, xa) : launch<fa::F16, false>(p, s, xa);
     return causal ? launch<fa::BF16, true>(p, s, xa) : launch<fa::BF16, false>(p, s, xa);
@@ -321,7 +335,7 @@ int dispatch_rope(const fa_rope_fwd_params *r, int dtype, int causal, void *stre
         return set_err(FA_ERR_INVALID_ARGUMENT, "RoPE tables must be 16-byte aligned with strides multiple of 8");
     if (r->rope_seqlen_stride < 0 || r->rope_seqlen_stride * 2 * fa::kQoSpanRows + 256 > 0x7fffffffLL)
         return set_err(FA_ERR_UNSUPPORTED, "RoPE seqlen stride too large for 32-bit tile offsets");
-    const fa::PathArgs ra{r->rope_cos, r->rope_sin, r->rope_batch_stride, r->rope_seqlen_stride, -1, 0, nullptr, nullptr};
+    const fa::PathArgs ra{r->rope_cos, r->rope_sin, r->rope_batch_stride, r->rope_seqlen_stride, -1, 0, nullptr, nullptr, nullptr, nullptr};
     hipStream_t s = (hipStream_t)stream;
     if (dtype == FA_DTYPE_F16)
         return causal ? launch<fa::F16, true>(r->base, s, ra) : launch<fa::F16, false>(r->base, s, ra);
@@ -345,7 +359,7 @@ int dispatch_window(const fa_fwd_params *params, int dtype, int causal, int64_t 
     }
     // the last query row's window starts at key Sk' - 1 - window_left: at or before 0, nothing is cut
     if (p.seqlen_kv - 1 <= window_left) return dispatch(&p, dtype, causal, nullptr, 0, stream);
-    const fa::PathArgs xa{nullptr, nullptr, 0, 0, (int)window_left, 0, nullptr, nullptr};
+    const fa::PathArgs xa{nullptr, nullptr, 0, 0, (int)window_left, 0, nullptr, nullptr, nullptr, nullptr};
     hipStream_t s = (hipStream_t)stream;
     if (dtype == FA_DTYPE_F16)
         return causal ? launch<fa::F16, true>(p, s, xa) : launch<fa::F16, false>(p, s, xa);
@@ -383,7 +397,7 @@ extern "C" int fa_fwd_gfx950_padded(const fa_padded_params *params, int dtype, i
 extern "C" int64_t fa_fwd_gfx950_padded_workspace_size(const fa_padded_params *params, int dtype, int causal,
                                                        int64_t window_left) {
     if (check_padded(params, dtype, causal) != FA_OK) return -1;
-    if (window_left >= 0 || params->q_range || !use_decode(params->base)) return padded_qfill_bytes(params, window_left);
+    if (!padded_on_decode(params, window_left)) return padded_rows_bytes(params);
     return fa::decode_ws_bytes(params->base, fa::decode_plan(params->base, fa::kDecMaxSplit));
 }
 

@@ -74,6 +74,8 @@ int64_t w4_grid(int64_t nwg);
 // ranges come with key ranges. Packed varlen passes cu_seqlens with rng_hi = 1
 // (fa_fwd_gfx950_varlen); padded batches [2, B] arrays of starts then ends with rng_hi = B
 // (fa_fwd_gfx950_padded). Masks are bottom-right aligned per sequence.
+// k_lo / k_hi (decode kernel only, fa_fwd_gfx950_padded): key POSITIONS [k_lo[b], k_hi[b]) within
+// batch row b (its batch strides apply), or nullptr.
 struct PathArgs {
     const void *cos;
     const void *sin;
@@ -82,6 +84,7 @@ struct PathArgs {
     int window_left;
     int rng_hi;
     const int *q_rng, *k_rng;
+    const int *k_lo, *k_hi;
 };
 
 // launch one (dtype, causal, head-dim tile, exact head dim) instantiation on `stream`
@@ -111,11 +114,9 @@ struct DecArgs {
     float *ws_o;    // [units * n_split][32][kD] fp32 partial O / l    (n_split > 1)
     float *ws_lse;  // [units * n_split][32] fp32 m * s' + log2(l)      (n_split > 1)
     int flags;      // kDec* bits
-    // per-sequence key ranges (PathArgs: absolute rows [k_rng[b], k_rng[b + rng_hi]) of k / v, whose
-    // batch strides the host zeroes), or nullptr (every key). Query ranges are not supported here
-    // (the dispatcher sends them to fa_fwd_w4).
-    int rng_hi;
-    const int *k_rng;
+    // per-sequence key positions [k_lo[b], k_hi[b]) within batch row b (a padded batch), or nullptr
+    // (every key). Query ranges are not supported here (the dispatcher sends them to fa_fwd_w4).
+    const int *k_lo, *k_hi;
 };
 constexpr int kDecNt = 1;  // K/V LDS-DMA with the non-temporal cache policy
 

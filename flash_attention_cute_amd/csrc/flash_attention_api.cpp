@@ -462,8 +462,9 @@ torch::Tensor flash_attention_padded_fwd(torch::Tensor &q, torch::Tensor &k, tor
     TORCH_CHECK(device_is_gfx950(q.device().index()),
                 "flash attention (gfx950 build) is only supported on MI355X / gfx950 devices");
 
-    // the kernels address a ranged tensor by absolute rows (row r at base + r * seqlen stride): the
-    // batch stride must be a multiple of the seqlen stride, the same multiple for k and v (q and o)
+    // the prefill kernel addresses a ranged sequence by absolute rows (row r at base + r * seqlen
+    // stride): the batch stride must be a multiple of the seqlen stride, the same multiple for k and v
+    // (q and o) -- other layouts are copied to a contiguous buffer
     auto rows_per_batch = [](const torch::Tensor &t) -> int64_t {
         if (t.size(0) == 1) return 0;
         if (t.stride(2) <= 0 || t.stride(0) % t.stride(2) != 0) return -1;
@@ -478,7 +479,11 @@ torch::Tensor flash_attention_padded_fwd(torch::Tensor &q, torch::Tensor &k, tor
     }
     int64_t head_q = qx.size(1), seqlen_q = qx.size(2);
     const int64_t head_kv = kx.size(1), headdim = qx.size(3), g = head_q / head_kv;
-    torch::Tensor ks = k_start, ke = k_end;
+    torch::Tensor ks = k_start.contiguous(), ke = k_end.contiguous(), qs, qe;
+    if (q_ranges) {
+        qs = q_start->contiguous();
+        qe = q_end->contiguous();
+    }
     // decode: one query row that sees the last window_left + 1 keys of its range -> narrow the range
     if (window_left >= 0 && seqlen_q == 1 && !q_ranges) {
         ks = torch::maximum(ks, ke - (int32_t)std::min<int64_t>(window_left + 1, 0x7fffffff));
@@ -493,21 +498,10 @@ torch::Tensor flash_attention_padded_fwd(torch::Tensor &q, torch::Tensor &k, tor
         qx = qx.reshape({bs, head_q, seqlen_q, headdim});
         if (!aligned16(qx)) qx = qx.contiguous();
     }
-    if (q_ranges && rows_per_batch(qx) < 0) qx = qx.contiguous();
+    if (!pack && rows_per_batch(qx) < 0) qx = qx.contiguous();  // (the prefill path may run)
     auto o = torch::empty_like(qx);
     if (!aligned16(o) || o.strides() != qx.strides()) o = torch::empty(qx.sizes(), qx.options());
     if (q_ranges) o.zero_();  // rows outside the query ranges are not written by the kernel
-
-    // [2, B] absolute rows: starts, then ends
-    const auto batch_idx = torch::arange(bs, k_start.options());
-    const int64_t rk = rows_per_batch(kx);
-    torch::Tensor k_range = torch::cat({ks + batch_idx * (int32_t)rk, ke + batch_idx * (int32_t)rk}).contiguous();
-    torch::Tensor q_range;
-    if (q_ranges) {
-        const int64_t rq = rows_per_batch(qx);
-        TORCH_CHECK(rows_per_batch(o) == rq, "internal: o rows differ from q rows");
-        q_range = torch::cat({*q_start + batch_idx * (int32_t)rq, *q_end + batch_idx * (int32_t)rq}).contiguous();
-    }
 
     fa_padded_params pp;
     fa_fwd_params &params = pp.base;
@@ -530,15 +524,17 @@ torch::Tensor flash_attention_padded_fwd(torch::Tensor &q, torch::Tensor &k, tor
     params.k_head_stride = stride_or_zero(kx, 1);
     params.v_head_stride = stride_or_zero(vx, 1);
     params.o_head_stride = stride_or_zero(o, 1);
-    // ranged tensors keep their seqlen stride even at size 1 (it converts rows into addresses)
-    params.q_seqlen_stride = q_ranges ? qx.stride(2) : stride_or_zero(qx, 2);
+    // the seqlen strides convert rows into addresses on the prefill path, even at size 1
+    params.q_seqlen_stride = pack ? stride_or_zero(qx, 2) : qx.stride(2);
     params.k_seqlen_stride = kx.stride(2);
     params.v_seqlen_stride = vx.stride(2);
-    params.o_seqlen_stride = q_ranges ? o.stride(2) : stride_or_zero(o, 2);
+    params.o_seqlen_stride = pack ? stride_or_zero(o, 2) : o.stride(2);
     softmax_scale *= M_LOG2E;
     params.softmax_scale = softmax_scale;
-    pp.q_range = q_ranges ? q_range.data_ptr<int32_t>() : nullptr;
-    pp.k_range = k_range.data_ptr<int32_t>();
+    pp.q_start = q_ranges ? qs.data_ptr<int32_t>() : nullptr;
+    pp.q_end = q_ranges ? qe.data_ptr<int32_t>() : nullptr;
+    pp.k_start = ks.data_ptr<int32_t>();
+    pp.k_end = ke.data_ptr<int32_t>();
 
     const int dtype = qx.scalar_type() == torch::kHalf ? FA_DTYPE_F16 : FA_DTYPE_BF16;
     void *stream = c10::hip::getCurrentHIPStream(qx.device().index()).stream();

@@ -180,28 +180,29 @@ int fa_fwd_gfx950_varlen_check(const fa_varlen_params *params, int dtype, int ca
  * (the reference drops attention_mask, models/rope_attn_fwd.py:40-64); this is the entry an HF
  * left- or right-padding mask is lowered to.
  *
- * `base` describes dense q [B, Hq, Sq, D], k/v [B, Hkv, Sk, D], o [B, Hq, Sq, D] as for
- * fa_fwd_gfx950 (seqlen_q / seqlen_kv = the padded lengths). Sequence b's real keys are ROWS
- * [k_range[b], k_range[B + b]) of k and v, counted from the base pointer in units of the seqlen
- * stride (row r of kv-head h at k_ptr + h * k_head_stride + r * k_seqlen_stride; for a tensor
- * whose batch stride is S times its seqlen stride, position s of batch row b is row b * S + s),
- * and its real queries rows [q_range[b], q_range[B + b]) of q and o likewise -- int32 [2, B] arrays
- * (B starts, then B ends) in DEVICE memory. The batch strides of a ranged tensor are not used.
- * q_range == NULL: every query row of batch row b (q / o batch strides apply); k_range == NULL:
- * every key (query ranges need key ranges). Masks are bottom-right aligned per sequence (key n of
- * the range visible to query m of the range iff n - k_start <= m - q_start + Sk_b - Sq_b);
- * window_left >= 0 adds the local window of fa_fwd_gfx950_window per sequence (< 0: none).
- * Output rows outside the query ranges are NOT written (the torch binding zero-fills them first);
- * rows with no visible key are 0. Few query rows per kv-head without query ranges or window (Sq ==
- * 1 after the q-head pack, or head_q_per_group * Sq <= 64) run the split-KV decode kernel on each
- * sequence's key rows, which wants fa_fwd_gfx950_padded_workspace_size() bytes of workspace to
- * split (NULL: unsplit), as fa_fwd_gfx950_ws. Asynchronous, no host synchronisation: safe under
- * hipGraph capture.
+ * `base` describes dense q [B, Hq, Sq, D], k/v [B, Hkv, Sk, D], o [B, Hq, Sq, D] exactly as for
+ * fa_fwd_gfx950 (seqlen_q / seqlen_kv = the padded lengths). Batch row b's real keys are positions
+ * [k_start[b], k_end[b]) of its Sk and its real queries positions [q_start[b], q_end[b]) of its Sq --
+ * int32 arrays of B entries in DEVICE memory; q_start == q_end == NULL means every query row,
+ * k_start == k_end == NULL every key. Masks are bottom-right aligned per sequence (key n of the
+ * range visible to query m of the range iff n - k_start <= m - q_start + Sk_b - Sq_b);
+ * window_left >= 0 adds the local window of fa_fwd_gfx950_window per sequence (< 0: none). Output
+ * rows outside the query ranges are NOT written (the torch binding zero-fills them first); rows with
+ * no visible key are 0.
+ * Few query rows per kv-head without query ranges or window (Sq == 1 after the q-head pack, or
+ * head_q_per_group * Sq <= 64) run the split-KV decode kernel on each sequence's key positions;
+ * everything else runs the prefill kernel, whose launch first converts the positions into row
+ * arrays in the workspace (this needs each tensor's batch stride to be a multiple of its seqlen
+ * stride, the same multiple for q and o, and for k and v). fa_fwd_gfx950_padded_workspace_size()
+ * gives the bytes either path wants (decode: split-KV partials, NULL = unsplit; prefill: required).
+ * Asynchronous, no host synchronisation: safe under hipGraph capture.
  */
 typedef struct fa_padded_params {
     fa_fwd_params base;
-    const int32_t *q_range; /* [2, B] first rows then end rows, device, or NULL */
-    const int32_t *k_range; /* [2, B] first rows then end rows, device, or NULL */
+    const int32_t *q_start; /* [B], device, or NULL */
+    const int32_t *q_end;   /* [B], device, or NULL */
+    const int32_t *k_start; /* [B], device, or NULL */
+    const int32_t *k_end;   /* [B], device, or NULL */
 } fa_padded_params;
 
 int fa_fwd_gfx950_padded(const fa_padded_params *params, int dtype, int causal, int64_t window_left,

@@ -294,11 +294,11 @@ def test_q_o_stride_bound_covers_the_interleaved_wave_slab(lib):
 
 
 class FaPaddedParams(ctypes.Structure):
-    _fields_ = [("base", FaFwdParams), ("q_range", ctypes.c_void_p), ("k_range", ctypes.c_void_p)]
+    _fields_ = [("base", FaFwdParams)] + [(n, ctypes.c_void_p) for n in ("q_start", "q_end", "k_start", "k_end")]
 
 
 def test_padded_struct_layout():
-    assert ctypes.sizeof(FaPaddedParams) == ctypes.sizeof(FaFwdParams) + 16
+    assert ctypes.sizeof(FaPaddedParams) == ctypes.sizeof(FaFwdParams) + 32
 
 
 def test_padded_entry_validates_before_touching_the_device(lib):
@@ -308,24 +308,26 @@ def test_padded_entry_validates_before_touching_the_device(lib):
     lib.fa_fwd_gfx950_padded_workspace_size.restype = ctypes.c_int64
     lib.fa_fwd_gfx950_padded_workspace_size.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64]
     lib.fa_last_error.restype = ctypes.c_char_p
-    # decode shape with key ranges: the split-KV plan of the dense call
-    dec = FaPaddedParams(decode_params(b=1, sk=32768), None, 0x50000)
+    # decode shape with key positions: the split-KV plan of the dense call
+    dec = FaPaddedParams(decode_params(b=1, sk=32768), None, None, 0x50000, 0x50100)
     assert lib.fa_fwd_gfx950_padded_workspace_size(ctypes.byref(dec), 0, 0, -1) == ws_size(lib, dec.base)
-    # prefill shape with key ranges only: 2 * B int32 query ranges derived in the workspace
-    pre = FaPaddedParams(good_params(), None, 0x50000)
-    assert lib.fa_fwd_gfx950_padded_workspace_size(ctypes.byref(pre), 0, 1, -1) == 16
-    assert lib.fa_fwd_gfx950_padded_workspace_size(ctypes.byref(pre), 0, 1, 100) == 16  # window: prefill kernel
-    both = FaPaddedParams(good_params(), 0x60000, 0x50000)
-    assert lib.fa_fwd_gfx950_padded_workspace_size(ctypes.byref(both), 0, 1, -1) == 0
-    # ... and refuses to launch without that workspace
+    # prefill shape: the [2, B] query and key row arrays (B = 2: 4 * 2 * 4 = 32 bytes)
+    pre = FaPaddedParams(good_params(), None, None, 0x50000, 0x50100)
+    assert lib.fa_fwd_gfx950_padded_workspace_size(ctypes.byref(pre), 0, 1, -1) == 32
+    assert lib.fa_fwd_gfx950_padded_workspace_size(ctypes.byref(dec), 0, 1, 100) == 16  # window: prefill kernel
+    # ... which refuses to launch without that workspace
     assert lib.fa_fwd_gfx950_padded(ctypes.byref(pre), 0, 1, -1, None, 0, None) == FA_ERR_INVALID_ARGUMENT
     assert b"workspace" in lib.fa_last_error()
-    qonly = FaPaddedParams(good_params(), 0x60000, None)
-    assert lib.fa_fwd_gfx950_padded(ctypes.byref(qonly), 0, 1, -1, None, 0, None) == FA_ERR_INVALID_ARGUMENT
-    assert b"key ranges" in lib.fa_last_error()
-    odd = FaPaddedParams(good_params(), None, 0x50002)
+    half = FaPaddedParams(good_params(), None, None, 0x50000, None)
+    assert lib.fa_fwd_gfx950_padded(ctypes.byref(half), 0, 1, -1, None, 0, None) == FA_ERR_INVALID_ARGUMENT
+    assert b"together" in lib.fa_last_error()
+    odd = FaPaddedParams(good_params(), None, None, 0x50002, 0x50100)
     assert lib.fa_fwd_gfx950_padded(ctypes.byref(odd), 0, 1, -1, None, 0, None) == FA_ERR_INVALID_ARGUMENT
-    bad = FaPaddedParams(good_params(headdim=136), None, 0x50000)
+    # prefill needs batch strides that are multiples of the seqlen strides (rows are addressed)
+    skew = FaPaddedParams(good_params(k_batch_stride=2 * 300 * 128 + 8), None, None, 0x50000, 0x50100)
+    rc = lib.fa_fwd_gfx950_padded(ctypes.byref(skew), 0, 1, -1, ctypes.c_void_p(0x70000), 32, None)
+    assert rc == FA_ERR_INVALID_ARGUMENT and b"multiple" in lib.fa_last_error()
+    bad = FaPaddedParams(good_params(headdim=136), None, None, 0x50000, 0x50100)
     assert lib.fa_fwd_gfx950_padded(ctypes.byref(bad), 0, 1, -1, None, 0, None) == FA_ERR_UNSUPPORTED
     assert lib.fa_fwd_gfx950_padded_workspace_size(ctypes.byref(bad), 0, 1, -1) == -1
     assert lib.fa_fwd_gfx950_padded(None, 0, 1, -1, None, 0, None) == FA_ERR_INVALID_ARGUMENT
