@@ -1260,8 +1260,15 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             // this gap's (independent) VALU above it, into the previous gap
             FA_SCHED_FENCE();
             if constexpr (ks + 1 < KS && i == 0) {
-                kf[cb ^ 1][0] = *(const u32x4 *)(K + k_addr[ks + 1]);
-                kf[cb ^ 1][1] = *(const u32x4 *)(K + 32 * RB + k_addr[ks + 1]);
+#ifdef FA_EXP_HALFLDS  // (timing experiment of the stamps build only: half the K fragment reads, wrong results)
+                if constexpr ((ks + 1) & 1) {
+                    asm volatile("" : "=v"(kf[cb ^ 1][0]), "=v"(kf[cb ^ 1][1]));
+                } else
+#endif
+                {
+                    kf[cb ^ 1][0] = *(const u32x4 *)(K + k_addr[ks + 1]);
+                    kf[cb ^ 1][1] = *(const u32x4 *)(K + 32 * RB + k_addr[ks + 1]);
+                }
             }
             if constexpr (do_dma && i == 2) {
                 if constexpr (ks < NP) dma_one_at<pr * T + ks * 1024>(kr, lds_base, kvo[ks], ks == 0);
@@ -1369,8 +1376,15 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             if constexpr (!(pdead && X == 0)) agpr_mfma<F, X * 16 * DTL + 16 * dt, true>(va[kk & 1][dt], P[cp][4 * X + kk]);
             FA_SCHED_FENCE();  // (see phase 1)
             if constexpr (kk + 1 < 4 && i < DTL) {
-                rd(kk + 1, 2 * i, va[(kk + 1) & 1]);
-                rd(kk + 1, 2 * i + 1, va[(kk + 1) & 1]);
+#ifdef FA_EXP_HALFLDS  // (timing experiment, as in phase 1: half the V^T fragment reads)
+                if constexpr ((kk + 1) & 1) {
+                    asm volatile("" : "=v"(va[(kk + 1) & 1][i]));
+                } else
+#endif
+                {
+                    rd(kk + 1, 2 * i, va[(kk + 1) & 1]);
+                    rd(kk + 1, 2 * i + 1, va[(kk + 1) & 1]);
+                }
             }
             // (kQPhase 2) the next block's Q pieces early in phase 2, where no K/V DMA is issued
             if constexpr (kQL == 2 && kQPhase == 2 && do_sm && g % 2 == 1 && g < 2 * kQPT) {
@@ -1739,7 +1753,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             o[7] = s_pro - st_t0;
             o[8] = s_end - s_masked_end;
             o[9] = rt_end - st_rt0;
-            o[10] = st_t0;
+            o[10] = st_rt0;  // (realtime: one clock for every XCD)
             o[11] = xcc_id();
         }
     }

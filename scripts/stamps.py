@@ -78,19 +78,27 @@ for i, nm in [(1, "p1"), (2, "p2+resc"), (3, "dma_wait"), (4, "barrier")]:
     print(f"  per tile {nm:10s} {float((s[:, i] / tiles).median()):8.0f} cycles")
 clk = (s[:, 0] / s[:, 9] * 100e6 / 1e9)
 print(f"  in-kernel clock median {float(clk.median()):.3f} GHz")
-start = s[:, 10] - s[:, 10].min()
-print(f"  launch span {float((s[:, 10] + s[:, 0]).max() - s[:, 10].min()):.0f} cycles, start spread "
-      f"{float(start.max()):.0f}")
-# whole-launch accounting (wave 0 of each Q block): busy share of the launch span over the grid's
-# workgroups (end-of-launch imbalance), and the share of the block switch in the busy cycles
+
+# whole-launch accounting in s_memrealtime ticks (100 MHz, one clock for all XCDs; record field 10 is
+# the block's realtime start, 9 its realtime duration), wave 0 of each Q block: busy share of the
+# launch span over the grid's workgroups (ramp-up and end-of-launch imbalance), per XCD too
 w0 = s[torch.arange(s.shape[0]) % WAVES == 0]
-span = float((w0[:, 10] + w0[:, 0]).max() - w0[:, 10].min())
+t_end = w0[:, 10] + w0[:, 9]
+span = float(t_end.max() - w0[:, 10].min())
 grid = min(nwg, 256)
-busy = float(w0[:, 0].sum())
+busy = float(w0[:, 9].sum())
 switch = float((w0[:, 6] + w0[:, 7] + w0[:, 8]).sum())
 loop = float((w0[:, 1] + w0[:, 2] + w0[:, 3] + w0[:, 4]).sum())
-print(f"  utilisation (busy / (span x {grid} workgroups)) {busy / (span * grid):.3f}; of the busy cycles: "
-      f"tiles {loop / busy:.3f}, switch (drain + prologue + epilogue) {switch / busy:.3f}")
+print(f"  launch span {span / 100:.1f} us; utilisation (busy / (span x {grid} workgroups)) {busy / (span * grid):.3f}; "
+      f"of the busy cycles: tiles {loop / float(w0[:, 0].sum()):.3f}, switch {switch / float(w0[:, 0].sum()):.3f}")
+first = float(w0[:, 10].min())
+print(f"  first block start spread {float(torch.quantile(w0[:, 10] - first, 0.99)) / 100:.2f} us (p99 over blocks), "
+      f"last end - p50 end of the XCDs' last blocks:")
+for x in range(8):
+    sel = w0[:, 11] == x
+    if sel.any():
+        e = t_end[sel]
+        print(f"    xcd {x}: blocks {int(sel.sum())}, end {float(e.max() - first) / 100:.1f} us")
 for i, nm in [(6, "drain"), (7, "prologue"), (8, "epilogue")]:
     qs = torch.quantile(s[:, i], torch.tensor([0.1, 0.5, 0.9, 0.99], dtype=torch.float64))
     print(f"  {nm:10s} p10 {qs[0]:8.0f}  p50 {qs[1]:8.0f}  p90 {qs[2]:8.0f}  p99 {qs[3]:8.0f}")
