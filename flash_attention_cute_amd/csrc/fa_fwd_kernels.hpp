@@ -1260,9 +1260,20 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             // this gap's (independent) VALU above it, into the previous gap
             FA_SCHED_FENCE();
             if constexpr (ks + 1 < KS && i == 0) {
-#ifdef FA_EXP_HALFLDS  // (timing experiment of the stamps build only: half the K fragment reads, wrong results)
+#if defined(FA_EXP_HALFLDS) || defined(FA_EXP_HALFK)  // (timing experiment of the stamps build only:
+                                                      // half the K fragment reads, wrong results)
                 if constexpr ((ks + 1) & 1) {
+#ifdef FA_EXP_HALF_XOR  // the skipped fragment: the previous one with mantissa bits flipped, so the MFMA
+                        // operands still toggle like real data (an opaque register is near-constant
+                        // data: the chip then clocks up for the data, not for the saved LDS reads)
+                    static_for<4>([&](auto E) {
+                        constexpr int e = decltype(E)::value;
+                        kf[cb ^ 1][0][e] = kf[cb][0][e] ^ 0x01ff01ffu;
+                        kf[cb ^ 1][1][e] = kf[cb][1][e] ^ 0x01ff01ffu;
+                    });
+#else
                     asm volatile("" : "=v"(kf[cb ^ 1][0]), "=v"(kf[cb ^ 1][1]));
+#endif
                 } else
 #endif
                 {
@@ -1376,9 +1387,16 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             if constexpr (!(pdead && X == 0)) agpr_mfma<F, X * 16 * DTL + 16 * dt, true>(va[kk & 1][dt], P[cp][4 * X + kk]);
             FA_SCHED_FENCE();  // (see phase 1)
             if constexpr (kk + 1 < 4 && i < DTL) {
-#ifdef FA_EXP_HALFLDS  // (timing experiment, as in phase 1: half the V^T fragment reads)
+#if defined(FA_EXP_HALFLDS) || defined(FA_EXP_HALFV)  // (timing experiment, as in phase 1: half the V^T reads)
                 if constexpr ((kk + 1) & 1) {
+#ifdef FA_EXP_HALF_XOR
+                    static_for<4>([&](auto E) {
+                        constexpr int e = decltype(E)::value;
+                        va[(kk + 1) & 1][i][e] = va[kk & 1][i][e] ^ 0x01ff01ffu;
+                    });
+#else
                     asm volatile("" : "=v"(va[(kk + 1) & 1][i]));
+#endif
                 } else
 #endif
                 {

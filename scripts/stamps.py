@@ -98,7 +98,10 @@ for x in range(8):
     sel = w0[:, 11] == x
     if sel.any():
         e = t_end[sel]
-        print(f"    xcd {x}: blocks {int(sel.sum())}, end {float(e.max() - first) / 100:.1f} us")
+        xs = w0[sel]
+        print(f"    xcd {x}: blocks {int(sel.sum())}, end {float(e.max() - first) / 100:.1f} us, "
+              f"busy {float(xs[:, 9].sum()) / 100:.0f} us, cycles {float(xs[:, 0].sum()) / 1e6:.2f} M, "
+              f"clock {float((xs[:, 0] / xs[:, 9]).median()) / 10:.3f} GHz")
 for i, nm in [(6, "drain"), (7, "prologue"), (8, "epilogue")]:
     qs = torch.quantile(s[:, i], torch.tensor([0.1, 0.5, 0.9, 0.99], dtype=torch.float64))
     print(f"  {nm:10s} p10 {qs[0]:8.0f}  p50 {qs[1]:8.0f}  p90 {qs[2]:8.0f}  p99 {qs[3]:8.0f}")
