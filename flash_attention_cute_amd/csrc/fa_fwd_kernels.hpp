@@ -1541,6 +1541,12 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             }
         }
     };
+    // does tile key0 hold a hidden score of rows row0..row0+31 (wave-uniform)? keys past the first
+    // row's last visible key (causal diagonal, Sk tail), or left of the last row's window
+    auto hides = [&](const int row0, const int key0) __attribute__((always_inline)) {
+        const int lim = kCausal ? min(Sk - 1, row0 + diag) : Sk - 1;
+        return key0 + kBlockN - 1 > lim || (wl >= 0 && key0 < row0 + 31 + diag - wl);
+    };
     // MASKED: 0 = no masked score, 1 = masked (diagonal / tail / window), 2 = masked and block A
     // dead in tile j (no row of any wave's block A sees a key of it), 3 = A dead in tiles j and j-1
     auto iter = [&](const int j, auto PAR, auto MASKED) __attribute__((always_inline)) {
@@ -1567,12 +1573,19 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #endif
 #ifndef FA_EXP_NOMASK  // (timing experiment of the stamps build only: no mask step, wrong results)
         if constexpr (mk != 0) {  // diagonal / tail tile: mask S before phase 2
+            // (per wave and block: only where some score of its 32 rows is hidden; on a causal
+            // diagonal that is half of the wave-blocks of the workgroup's masked tiles)
+            const int key0 = j * kBlockN;
             if constexpr (mk == 1) {
-                s_ready(S[c][0], S[c][1]);
-                mask(S[c][0], S[c][1], mw, j * kBlockN);
+                if (hides(mw, key0)) {
+                    s_ready(S[c][0], S[c][1]);
+                    mask(S[c][0], S[c][1], mw, key0);
+                }
             }
-            s_ready(S[c][2], S[c][3]);
-            mask(S[c][2], S[c][3], mw + kRowB, j * kBlockN);
+            if (hides(mw + kRowB, key0)) {
+                s_ready(S[c][2], S[c][3]);
+                mask(S[c][2], S[c][3], mw + kRowB, key0);
+            }
         }
 #endif
         FA_STAMP(sb);
