@@ -761,6 +761,55 @@ __device__ __forceinline__ void dma_pieces(const rsrc_t &rs, const uint32_t lds0
 #pragma unroll
     for (int n = 0; n < NP; ++n) dma_one(rs, lds0 + n * 1024, voff[n], n == 0);
 }
+
+// A K / V tile descriptor as four plain SGPR words -- base lo, base hi (stride 0, no swizzle, so the
+// word is the address's high half), num_records, flags -- that fa_fwd_w4's tile loop advances in
+// place (s_add_u32 / s_addc_u32) instead of re-assembling a descriptor per tile.
+__device__ __forceinline__ u32x4 make_quad(const char *base, uint32_t nbytes) {
+    const uint64_t a = (uint64_t)(uintptr_t)base;
+    return (u32x4){(uint32_t)a, (uint32_t)(a >> 32), nbytes, 0x00020000u};
+}
+__device__ __forceinline__ void quad_advance(u32x4 &q, const int64_t step) {
+    const uint64_t a = (((uint64_t)q[1] << 32) | q[0]) + (uint64_t)step;
+    q[0] = (uint32_t)a;
+    q[1] = (uint32_t)(a >> 32);
+}
+// One LDS-DMA piece of a tile from descriptor q + voff + IOFF to LDS M0 + IOFF: gfx950 adds the
+// instruction offset to the LDS destination as well as to the source (scripts/microbench/
+// ldsdma_offset.hip), so the pieces n = 1.. of a tile reuse piece 0's M0 with IOFF = n * 1024 and
+// voff pre-reduced by n * 1024 (same bytes, same bounds check: the offset is range-checked).
+// Piece 0 (IOFF == 0) writes M0 = m0v (+ one wait state before the LDS-DMA reads it); nothing
+// between the pieces of one tile may write M0 (the loop issues no other LDS-DMA in that phase).
+template <int IOFF>
+__device__ __forceinline__ void dma_q(const u32x4 &q, const uint32_t m0v, const int voff) {
+    if constexpr (IOFF == 0)
+        asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(q),
+                     "s"(m0v)
+                     : "memory", "m0");
+    else
+        asm volatile("buffer_load_dwordx4 %0, %1, 0 offen offset:%2 lds" ::"v"(voff), "s"(q), "i"(IOFF) : "memory");
+}
+// the NP pieces of one tile outside the pipelined loop: every piece names M0 as an input (hipcc
+// sets it) and carries its own wait state
+template <int NP, int N = 0>
+__device__ __forceinline__ void dma_tile(const u32x4 &q, const uint32_t m0v, const int *voff) {
+    if constexpr (N < NP) {
+        asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen offset:%3 lds" ::"v"(voff[N]), "s"(q), "{m0}"(m0v),
+                     "i"(N * 1024)
+                     : "memory");
+        dma_tile<NP, N + 1>(q, m0v, voff);
+    }
+}
+// the same with M0 = base + MOFF formed inside the asm (one LDS base SGPR for every slot)
+template <int MOFF, int IOFF>
+__device__ __forceinline__ void dma_q_at(const u32x4 &q, const uint32_t base, const int voff) {
+    if constexpr (IOFF == 0)
+        asm volatile("s_add_u32 m0, %2, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(q),
+                     "s"(base), "i"(MOFF)
+                     : "memory", "m0", "scc");
+    else
+        asm volatile("buffer_load_dwordx4 %0, %1, 0 offen offset:%2 lds" ::"v"(voff), "s"(q), "i"(IOFF) : "memory");
+}
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // s_waitcnt immediate for vmcnt(n) alone (gfx9 encoding: vmcnt[3:0] + vmcnt[5:4] at [15:14], expcnt
 // 7, lgkmcnt 15)
@@ -834,6 +883,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #define FA_QPH 2
 #endif
     constexpr int kQPhase = FA_QPH;  // phase of the tile that issues them
+    // (phase 1's K / V pieces share one M0 per tensor, dma_q_at: no other LDS-DMA may sit between them)
+    static_assert(kQL != 2 || kQPhase == 2, "Q pieces in phase 2 only");
     constexpr int NQP = T / 1024;  // Q pieces per wave (its 64 rows): 16 / 8
     // a wave's block B starts kRowB rows after its block A (rows interleaved over the waves); the
     // wave's rows span kRowSpan rows from mw
@@ -1058,19 +1109,23 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         const int slot = ((16 * lane) % RB) / 16;
         const int kch = G::k_off(row, slot) % RB / 16;  // the XOR swizzles are involutions
         const int vch = G::v_off(row, slot) % RB / 16;
-        kvo[n] = (kExactD || kch * 8 < D) ? row * ks_ * 2 + 16 * kch : 0x7ffffff0;
-        vvo[n] = (kExactD || vch * 8 < D) ? row * vs_ * 2 + 16 * vch : 0x7ffffff0;
+        // piece n is issued with instruction offset n * 1024 (dma_q): its lane offsets carry
+        // -n * 1024 (row >= n * ROWS_PER_PIECE and the row stride >= D keep them >= 0)
+        kvo[n] = ((kExactD || kch * 8 < D) ? row * ks_ * 2 + 16 * kch : 0x7ffffff0) - n * 1024;
+        vvo[n] = ((kExactD || vch * 8 < D) ? row * vs_ * 2 + 16 * vch : 0x7ffffff0) - n * 1024;
     }
-    // tile j into ring slot `slot` (the block's tiles alternate slots from j_lo on)
-    auto stage_k = [&](const int j, const int slot) {
+    // tile j into ring slot `slot` (the block's tiles alternate slots from j_lo on), outside the
+    // pipelined loop: every piece names M0 as an input (hipcc sets it; one wait state in the asm)
+    auto stage_pieces = [&](const char *base, const int stride, const int j, const uint32_t m0v, const int *voff) {
         const int key0 = j * kBlockN;
-        const rsrc_t kr = make_rsrc(kb + 2 * (int64_t)key0 * ks_, slab_bytes(min(Sk - key0, kBlockN), ks_, D));
-        dma_pieces<NP>(kr, lds_u32(lds + KV0 + slot * T) + wave * NP * 1024, kvo);
+        dma_tile<NP>(make_quad(base + 2 * (int64_t)key0 * stride, slab_bytes(min(Sk - key0, kBlockN), stride, D)), m0v,
+                     voff);
+    };
+    auto stage_k = [&](const int j, const int slot) {
+        stage_pieces(kb, ks_, j, lds_u32(lds + KV0 + slot * T) + wave * NP * 1024, kvo);
     };
     auto stage_v = [&](const int j, const int slot) {
-        const int key0 = j * kBlockN;
-        const rsrc_t vr = make_rsrc(vb + 2 * (int64_t)key0 * vs_, slab_bytes(min(Sk - key0, kBlockN), vs_, D));
-        dma_pieces<NP>(vr, lds_u32(lds + KV0 + (2 + slot) * T) + wave * NP * 1024, vvo);
+        stage_pieces(vb, vs_, j, lds_u32(lds + KV0 + (2 + slot) * T) + wave * NP * 1024, vvo);
     };
 
     // ---- per-lane LDS read addresses -----------------------------------------------------
@@ -1237,7 +1292,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     constexpr int G1 = 4 * KS;
     // AD (A-dead tiles, causal diagonal): bit 0 = block A has no visible score in this tile (its S
     // MFMAs are skipped), bit 1 = nor in the previous tile (its late softmax units are skipped)
-    auto phase1 = [&](const char *K, auto PAR, auto SM2, auto DMA, const rsrc_t &kr, const rsrc_t &vr, auto AD)
+    auto phase1 = [&](const char *K, auto PAR, auto SM2, auto DMA, const u32x4 &kq, const u32x4 &vq, auto AD)
         __attribute__((always_inline)) {
         constexpr int c = decltype(PAR)::value, pr = c ^ 1;
         constexpr bool do_sm = decltype(SM2)::value, do_dma = decltype(DMA)::value;
@@ -1282,8 +1337,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                 }
             }
             if constexpr (do_dma && i == 2) {
-                if constexpr (ks < NP) dma_one_at<pr * T + ks * 1024>(kr, lds_base, kvo[ks], ks == 0);
-                else dma_one_at<(2 + c) * T + (ks - NP) * 1024>(vr, lds_base, vvo[ks - NP], ks == NP);
+                if constexpr (ks < NP) dma_q_at<pr * T, ks * 1024>(kq, lds_base, kvo[ks]);
+                else dma_q_at<(2 + c) * T, (ks - NP) * 1024>(vq, lds_base, vvo[ks - NP]);
             }
             // the next block's Q: kQPT pieces per tile, in evenly spaced gaps
             if constexpr (kQL == 2 && kQPhase == 1 && do_dma && i == 3 && (ks * kQPT) % KS == 0) {
@@ -1454,19 +1509,14 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         });
     };
 
-    auto k_rsrc = [&](const int j) {
-        const int key0 = j * kBlockN;
-        return make_rsrc(kb + 2 * (int64_t)key0 * ks_, slab_bytes(min(Sk - key0, kBlockN), ks_, D));
-    };
-    auto v_rsrc = [&](const int j) {
-        const int key0 = j * kBlockN;
-        return make_rsrc(vb + 2 * (int64_t)key0 * vs_, slab_bytes(min(Sk - key0, kBlockN), vs_, D));
-    };
-    // pipelined loop: running tile pointers (no 64-bit multiply per tile); a full tile spans
-    // full_k / full_v bytes, the Sk tail tile fewer, a tile past Sk none
+    // pipelined loop: the K_{j+1} / V_j descriptors are SGPR quads advanced in place (no 64-bit
+    // multiply nor descriptor assembly per tile); a full tile spans full_k / full_v bytes, the Sk
+    // tail tile fewer, a tile past Sk none
     const uint32_t full_k = slab_bytes(kBlockN, ks_, D), full_v = slab_bytes(kBlockN, vs_, D);
     const int64_t step_k = 2 * (int64_t)kBlockN * ks_, step_v = 2 * (int64_t)kBlockN * vs_;
-    const char *kp, *vp;  // K tile j + 1 / V tile j of iteration j
+    u32x4 kq, vq;       // K tile j + 1 / V tile j of iteration j
+    int kfe = 0;        // tiles below kfe are full (this block's Sk)
+    uint32_t k_last = 0;  // the bytes of K tile kfe (the Sk tail, or 0)
     auto tile_bytes = [&](const int key0, const uint32_t full, const int stride) {
         const int rows = Sk - key0;
         return rows >= kBlockN ? full : slab_bytes(rows, stride, D);
@@ -1481,8 +1531,10 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #pragma unroll
     for (int i = 0; i < 8; ++i) st_acc[i] = 0;
 #endif
-    kp = kb + (j_lo + 1) * step_k;
-    vp = vb + j_lo * step_v;
+    kq = make_quad(kb + (j_lo + 1) * step_k, 0u);
+    vq = make_quad(vb + j_lo * step_v, 0u);
+    kfe = Sk / kBlockN;
+    k_last = tile_bytes(kfe * kBlockN, full_k, ks_);
     if (rope_q) load_q_rope();
 #pragma unroll
     for (int X = 0; X < 2; ++X) {
@@ -1559,18 +1611,23 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             st[0].t = 0.f;
         }
         FA_STAMP(sa);
-        const rsrc_t kr = make_rsrc(kp, tile_bytes((j + 1) * kBlockN, full_k, ks_));
-        const rsrc_t vr = make_rsrc(vp, tile_bytes(j * kBlockN, full_v, vs_));
-        kp += step_k;
-        vp += step_v;
+        if constexpr (mk == 0) {  // unmasked: j + 1 <= n_pipe <= kfe, V_j full
+            kq[2] = j + 1 < kfe ? full_k : k_last;
+            vq[2] = full_v;
+        } else {
+            kq[2] = tile_bytes((j + 1) * kBlockN, full_k, ks_);
+            vq[2] = tile_bytes(j * kBlockN, full_v, vs_);
+        }
         // FA_EXP_*: timing experiments of the stamps build only (results are garbage)
 #if defined(FA_EXP_NOSM)
-        phase1(lds + KV0 + c * T, PAR, IC<0>{}, IC<1>{}, kr, vr, AD{});
+        phase1(lds + KV0 + c * T, PAR, IC<0>{}, IC<1>{}, kq, vq, AD{});
 #elif defined(FA_EXP_NODMA)
-        phase1(lds + KV0 + c * T, PAR, IC<1>{}, IC<0>{}, kr, vr, AD{});
+        phase1(lds + KV0 + c * T, PAR, IC<1>{}, IC<0>{}, kq, vq, AD{});
 #else
-        phase1(lds + KV0 + c * T, PAR, IC<1>{}, IC<1>{}, kr, vr, AD{});
+        phase1(lds + KV0 + c * T, PAR, IC<1>{}, IC<1>{}, kq, vq, AD{});
 #endif
+        quad_advance(kq, step_k);
+        quad_advance(vq, step_v);
 #ifndef FA_EXP_NOMASK  // (timing experiment of the stamps build only: no mask step, wrong results)
         if constexpr (mk != 0) {  // diagonal / tail tile: mask S before phase 2
             // (per wave and block: only where some score of its 32 rows is hidden; on a causal
@@ -1677,7 +1734,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         const char *K = lds + KV0 + sl * T;
         const char *V = lds + KV0 + (2 + sl) * T;
         const int key0 = j * kBlockN;
-        phase1(K, IC<0>{}, IC<0>{}, IC<0>{}, k_rsrc(j), k_rsrc(j), IC<0>{});
+        phase1(K, IC<0>{}, IC<0>{}, IC<0>{}, kq, vq, IC<0>{});  // (no DMA: the descriptors are unused)
         s_ready(S[0][0], S[0][1]);
         s_ready(S[0][2], S[0][3]);
         mask(S[0][0], S[0][1], mw, key0);
