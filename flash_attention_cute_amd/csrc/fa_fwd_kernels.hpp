@@ -91,7 +91,6 @@ struct F16 {
         f16x2 v = __builtin_convertvector((f32x2){lo, hi}, f16x2);
         return __builtin_bit_cast(uint32_t, v);
     }
-    // 8 values * s in fp32, rounded back (RNE)
     // rotate-half RoPE of 8 elements (HF apply_rotary_pos_emb, reference models/rope_attn_fwd.py:8-38):
     // x*cos + rot*sin with rot = -partner (first half) / +partner (second half), fp32, one RNE rounding
     static __device__ __forceinline__ u32x4 rope8(u32x4 v, u32x4 partner, u32x4 c, u32x4 s, bool second) {
@@ -107,13 +106,6 @@ struct F16 {
             asm volatile("" : "+v"(a0), "+v"(a1));  // fp32 rounding step kept, as csrc/fa_rope.hip
             r[i] = pack(a0, a1);
         }
-        return r;
-    }
-    static __device__ __forceinline__ u32x4 scale8(u32x4 v, float s) {
-        const f16x8 x = __builtin_bit_cast(f16x8, v);
-        u32x4 r;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) r[i] = pack((float)x[2 * i] * s, (float)x[2 * i + 1] * s);
         return r;
     }
 };
@@ -144,13 +136,6 @@ struct BF16 {
             asm volatile("" : "+v"(a0), "+v"(a1));  // fp32 rounding step kept, as csrc/fa_rope.hip
             r[i] = pack(a0, a1);
         }
-        return r;
-    }
-    static __device__ __forceinline__ u32x4 scale8(u32x4 v, float s) {
-        const bf16x8 x = __builtin_bit_cast(bf16x8, v);
-        u32x4 r;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) r[i] = pack((float)x[2 * i] * s, (float)x[2 * i + 1] * s);
         return r;
     }
 };
@@ -654,15 +639,6 @@ __device__ __forceinline__ void agpr_qlds(const uint32_t addr) {
     FA_CASE(160) FA_CASE(164) FA_CASE(168) FA_CASE(172) FA_CASE(176) FA_CASE(180) FA_CASE(184) FA_CASE(188)
 #undef FA_CASE
 }
-// first k-step with C = bias (the running reference max, kFoldScale)
-template <bool kF16, int QB>
-__device__ __forceinline__ void mfma_sq_bias(f32x16 &acc, const u32x4 &a, const f32x16 &bias) {
-#define FA_CASE(N) \
-    if constexpr (QB == N) { if constexpr (kF16) fa_sq_f16_##N##_b(acc, a, bias); else fa_sq_bf16_##N##_b(acc, a, bias); }
-    FA_CASE(128) FA_CASE(132) FA_CASE(136) FA_CASE(140) FA_CASE(144) FA_CASE(148) FA_CASE(152) FA_CASE(156)
-    FA_CASE(160) FA_CASE(164) FA_CASE(168) FA_CASE(172) FA_CASE(176) FA_CASE(180) FA_CASE(184) FA_CASE(188)
-#undef FA_CASE
-}
 template <bool kF16, int QB>
 __device__ __forceinline__ void mfma_sq(const bool first, f32x16 &acc, const u32x4 &a) {
 #define FA_CASE(N)                                                                         \
@@ -846,15 +822,6 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #endif
     using G = Geo<kD>;
     constexpr bool F = DT::kIsF16;
-#ifndef FA_FOLD
-    constexpr bool kFold = false;
-#else
-    // (experiment, off: +32 VGPRs of bias push the kernel past 256 arch VGPRs and it measured
-    // slower) Q is pre-scaled by s' = scale*log2(e) (fp32 multiply, rounded to T once per workgroup) and
-    // the first k-step of S = K.Q^T accumulates from C = -m*s' (the running reference max,
-    // "bias"): S is then already the exp2 argument and a score costs no fma
-    constexpr bool kFold = true;
-#endif
     constexpr int KS = G::kKSteps;
     constexpr int DTL = G::kDTiles;
     constexpr int RB = G::kRowBytes;
@@ -1002,20 +969,10 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             const bool ok = kExactD || 16 * ks + 8 * h < D;  // columns past D read as 0
             return ok ? (kRowB * X + r) * qs * 2 + 32 * ks + 16 * h : 0x7ffffff0;
         };
-        if constexpr (kFold) {
-            u32x4 qv[2 * KS];
-#pragma unroll
-            for (int X = 0; X < 2; ++X)
-#pragma unroll
-                for (int ks = 0; ks < KS; ++ks)
-                    qv[X * KS + ks] = DT::scale8(__builtin_amdgcn_raw_buffer_load_b128(qr, qoff(X, ks), 0, 0), sc);
-            static_for<2 * KS>([&](auto I) { agpr_qset<QB + 4 * decltype(I)::value>(qv[decltype(I)::value]); });
-        } else {
-            static_for<2 * KS>([&](auto I) {
-                constexpr int i = decltype(I)::value;
-                agpr_qload<QB + 4 * i>(qr, qoff(i / KS, i % KS), i == 0);
-            });
-        }
+        static_for<2 * KS>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            agpr_qload<QB + 4 * i>(qr, qoff(i / KS, i % KS), i == 0);
+        });
     };
     // RoPE fused into the Q load (xa.cos != nullptr, exact D): Q, cos and sin of the wave's 64 rows
     // into VGPRs, rotate-half in fp32, rounded once to T, then into the Q AGPRs. The rotation partner
@@ -1151,17 +1108,15 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     bool q_in_agpr = false;  // the block's Q was read into the AGPRs at the switch
     // ---- state ------------------------------------------------------------------------------
     struct Sm {               // online-softmax state of one block (per lane: one query row)
-        float m, msc, alpha;  // running max (unscaled), m*sc, alpha of the last decision
+        float m, nmsc, alpha;  // running max (unscaled), -m*sc (the exp2 argument's addend: no
+                               // negation per tile), alpha of the last decision
         float mt;             // m + the rescale threshold (unscaled)
         float mE, mO;         // two max chains over the tile being reduced (mE then holds m_new)
         float l, t;           // this lane's half of the row sum over finished tiles; s0 sum of the
-                              // tile being reduced (new scale, folded into l at the rescale)
-        float delta;          // kFold: rise of the reference m*sc at this tile's decision
+                              // tile being reduced (new scale, added to l at the end of the tile)
         uint64_t rmask;       // the decision's ballot (rows whose max outgrew m + threshold)
-        bool resc, seen, vis; // kFold: the row has seen a visible key; this tile has one
     };
     Sm st[2];
-    f32x16 bias[2];  // kFold: -m*s' per lane, the C operand of the first S k-step
     f32x16 S[2][4];  // [tile parity][2 * block + half]: half 0 = keys 0-31, 1 = keys 32-63
     u32x4 P[2][8];   // [tile parity][4 * block + k-step]
 
@@ -1177,34 +1132,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     auto u_dec = [&](const int c, const int X, const int k) {
         Sm &Z = st[X];
 #ifdef FA_EXP_NODEC
-        if (true) { (void)c; (void)k; Z.resc = false; Z.alpha = 1.f; return; }  // timing only
+        if (true) { (void)c; (void)k; Z.rmask = 0; return; }  // timing only
 #endif
-        if constexpr (kFold) {
-            // S already holds s*s' - m*s' (bias): the tile max is the rise over the reference
-            if (k == 0) {
-                const float mx = pair_max(fmaxf(Z.mE, Z.mO));
-                Z.vis = mx > 0.5f * kNeg;
-                const bool grow = Z.seen ? (mx > kRescaleThr) : Z.vis;
-                Z.resc = __builtin_amdgcn_ballot_w64(grow) != 0;
-                // first visible key: the reference jumps to the tile max (any sign); later only up
-                Z.delta = Z.resc ? (Z.seen ? fmaxf(mx, 0.f) : (Z.vis ? mx : 0.f)) : 0.f;
-                pin(Z.delta);
-            } else {
-                Z.alpha = Z.resc ? (Z.seen ? __builtin_amdgcn_exp2f(-Z.delta) : 0.f) : 1.f;
-                Z.seen = Z.seen || Z.vis;
-                pin(Z.alpha);
-                if (Z.resc) {  // rare: shift this tile's scores and the bias to the new reference
-                    Z.msc += Z.delta;
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        S[c][2 * X][i] -= Z.delta;
-                        S[c][2 * X + 1][i] -= Z.delta;
-                        bias[X][i] = -Z.msc;
-                    }
-                }
-            }
-            return;
-        }
         if (k == 0) {
             // both lane halves hold the same row's m, so the ballot over the half-row maxima
             // needs no cross-half reduction; the row max itself is only needed to rescale
@@ -1214,7 +1143,6 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             uint64_t bm = __builtin_amdgcn_ballot_w64(mx > Z.mt);
             asm volatile("" : "+s"(bm));
             Z.rmask = bm;
-            Z.resc = bm != 0;
             Z.mE = mx;
             pin(Z.mE);
         } else if (__builtin_expect(Z.rmask != 0, 0)) {  // wave-uniform and rare: the rest only then
@@ -1222,11 +1150,11 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             const float seen = m_new > 0.5f * kNeg ? 1.f : 0.f;  // m_new * sc, or 0 before any visible key
             const float msc_new = m_new * sc * seen;
             // a row's first visible key: O and l are still 0 and exp2(0 - m*sc) may overflow
-            Z.alpha = (Z.m <= 0.5f * kNeg) ? 0.f : __builtin_amdgcn_exp2f(Z.msc - msc_new);
+            Z.alpha = (Z.m <= 0.5f * kNeg) ? 0.f : __builtin_amdgcn_exp2f(-Z.nmsc - msc_new);
             Z.m = m_new;
             Z.mt = m_new + thr_raw;
-            Z.msc = msc_new;
-            pin(Z.msc);
+            Z.nmsc = -msc_new;
+            pin(Z.nmsc);
             pin(Z.alpha);
         }
     };
@@ -1234,9 +1162,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     auto u_exp = [&](const int c, const int X, const int hf, const int v) {
         f32x16 &s = S[c][2 * X + hf];
 #if defined(FA_EXP_NOEXP)
-        float x = __builtin_fmaf(s[v], sc, -st[X].msc);
+        float x = __builtin_fmaf(s[v], sc, st[X].nmsc);
 #else
-        float x = kFold ? __builtin_amdgcn_exp2f(s[v]) : __builtin_amdgcn_exp2f(__builtin_fmaf(s[v], sc, -st[X].msc));
+        float x = __builtin_amdgcn_exp2f(__builtin_fmaf(s[v], sc, st[X].nmsc));
 #endif
         pin(x);
         s[v] = x;
@@ -1247,9 +1175,12 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         const f32x16 &s = S[c][2 * X + hf];
         {
             // the late scores (run after the tile's rescale) add into l, the early ones into t
+            // (t restarts every tile: seeded with s[0] + s[1] at v == 1, no copy at v == 0)
             float &acc = (16 * hf + v >= kV0) ? st[X].l : st[X].t;
-            acc = (hf == 0 && v == 0) ? s[0] : acc + s[v];
-            pin(acc);
+            if (!(hf == 0 && v == 0)) {
+                acc = (hf == 0 && v == 1) ? s[0] + s[1] : acc + s[v];
+                pin(acc);
+            }
         }
         if (v & 1) {
             uint32_t w = DT::pack(s[v - 1], s[v]);
@@ -1306,8 +1237,6 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             // one counted wait per k-step (its two K fragments were read a whole k-step ahead)
             if constexpr (ks > 0 && i == 0) __builtin_amdgcn_s_waitcnt(kLgkm0);
             if constexpr (sdead && i < 2) {
-            } else if constexpr (kFold && ks == 0) {
-                mfma_sq_bias<F, QB + 4 * ((i >> 1) * KS + ks)>(S[c][i], kf[cb][i & 1], bias[i >> 1]);
             } else {
                 mfma_sq<F, QB + 4 * ((i >> 1) * KS + ks)>(ks == 0, S[c][i], kf[cb][i & 1]);
             }
@@ -1461,7 +1390,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             }
             // (kQPhase 2) the next block's Q pieces early in phase 2, where no K/V DMA is issued
             if constexpr (kQL == 2 && kQPhase == 2 && do_sm && g % 2 == 1 && g < 2 * kQPT) {
-                if (qn < qnt) {
+                if (__builtin_expect(qn < qnt, 0)) {  // (out of line: the common path falls through)
                     q_piece(qnr, qn);
                     ++qn;
                 }
@@ -1538,8 +1467,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     if (rope_q) load_q_rope();
 #pragma unroll
     for (int X = 0; X < 2; ++X) {
-        st[X] = {kNeg, 0.f, 1.f, kNeg + thr_raw, kNeg, kNeg, 0.f, 0.f, 0.f, 0ull, false, false, false};
-        bias[X] = (f32x16){};
+        st[X] = {kNeg, 0.f, 1.f, kNeg + thr_raw, kNeg, kNeg, 0.f, 0.f, 0ull};
     }
     if constexpr (DTL == 4) fa_agpr_zero_4(); else fa_agpr_zero_2();
     // tile -1 of the pipeline is empty: its S = kNeg gives P = 0, and its P.V reads V slot 1,
@@ -1607,7 +1535,6 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         using AD = IC<mk == 2 ? 1 : mk == 3 ? 3 : 0>;
         if constexpr (mk >= 2) {  // block A takes no decision and adds no row sum in tile j
             st[0].rmask = 0;
-            st[0].resc = false;
             st[0].t = 0.f;
         }
         FA_STAMP(sa);
