@@ -738,49 +738,44 @@ __device__ __forceinline__ void dma_pieces(const rsrc_t &rs, const uint32_t lds0
     for (int n = 0; n < NP; ++n) dma_one(rs, lds0 + n * 1024, voff[n], n == 0);
 }
 
-// A K / V tile descriptor as four plain SGPR words -- base lo, base hi (stride 0, no swizzle, so the
-// word is the address's high half), num_records, flags -- that fa_fwd_w4's tile loop advances in
-// place (s_add_u32 / s_addc_u32) instead of re-assembling a descriptor per tile.
-__device__ __forceinline__ u32x4 make_quad(const char *base, uint32_t nbytes) {
-    const uint64_t a = (uint64_t)(uintptr_t)base;
-    return (u32x4){(uint32_t)a, (uint32_t)(a >> 32), nbytes, 0x00020000u};
-}
-__device__ __forceinline__ void quad_advance(u32x4 &q, const int64_t step) {
-    const uint64_t a = (((uint64_t)q[1] << 32) | q[0]) + (uint64_t)step;
-    q[0] = (uint32_t)a;
-    q[1] = (uint32_t)(a >> 32);
-}
 // One LDS-DMA piece of a tile from descriptor q + voff + IOFF to LDS M0 + IOFF: gfx950 adds the
 // instruction offset to the LDS destination as well as to the source (scripts/microbench/
 // ldsdma_offset.hip), so the pieces n = 1.. of a tile reuse piece 0's M0 with IOFF = n * 1024 and
 // voff pre-reduced by n * 1024 (same bytes, same bounds check: the offset is range-checked).
-// Piece 0 (IOFF == 0) writes M0 = m0v (+ one wait state before the LDS-DMA reads it); nothing
-// between the pieces of one tile may write M0 (the loop issues no other LDS-DMA in that phase).
+// Piece 0 (IOFF == 0) writes M0 = m0v, then 5 wait states before the LDS-DMA (1 for the SALU
+// write of M0, 5 if hipcc produced the descriptor by a VALU write of SGPRs, e.g. v_readfirstlane:
+// the hazard recognizer does not see this asm read them); nothing between the pieces of one tile
+// may write M0 (the loop issues no other LDS-DMA in that phase).
 template <int IOFF>
-__device__ __forceinline__ void dma_q(const u32x4 &q, const uint32_t m0v, const int voff) {
+__device__ __forceinline__ void dma_q(const rsrc_t &q, const uint32_t m0v, const int voff) {
     if constexpr (IOFF == 0)
-        asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(q),
+        asm volatile("s_mov_b32 m0, %2\n\ts_nop 4\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(q),
                      "s"(m0v)
                      : "memory", "m0");
     else
         asm volatile("buffer_load_dwordx4 %0, %1, 0 offen offset:%2 lds" ::"v"(voff), "s"(q), "i"(IOFF) : "memory");
 }
 // the NP pieces of one tile outside the pipelined loop: every piece names M0 as an input (hipcc
-// sets it) and carries its own wait state
+// sets it) and carries its own wait states (5 ahead of the first: the descriptor may come from a
+// v_readfirstlane, a VALU write of SGPRs that the hazard recognizer cannot see the asm read)
 template <int NP, int N = 0>
-__device__ __forceinline__ void dma_tile(const u32x4 &q, const uint32_t m0v, const int *voff) {
+__device__ __forceinline__ void dma_tile(const rsrc_t &q, const uint32_t m0v, const int *voff) {
     if constexpr (N < NP) {
-        asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen offset:%3 lds" ::"v"(voff[N]), "s"(q), "{m0}"(m0v),
-                     "i"(N * 1024)
-                     : "memory");
+        if constexpr (N == 0)
+            asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff[N]), "s"(q), "{m0}"(m0v)
+                         : "memory");
+        else
+            asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen offset:%3 lds" ::"v"(voff[N]), "s"(q),
+                         "{m0}"(m0v), "i"(N * 1024)
+                         : "memory");
         dma_tile<NP, N + 1>(q, m0v, voff);
     }
 }
 // the same with M0 = base + MOFF formed inside the asm (one LDS base SGPR for every slot)
 template <int MOFF, int IOFF>
-__device__ __forceinline__ void dma_q_at(const u32x4 &q, const uint32_t base, const int voff) {
+__device__ __forceinline__ void dma_q_at(const rsrc_t &q, const uint32_t base, const int voff) {
     if constexpr (IOFF == 0)
-        asm volatile("s_add_u32 m0, %2, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(q),
+        asm volatile("s_add_u32 m0, %2, %3\n\ts_nop 4\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(q),
                      "s"(base), "i"(MOFF)
                      : "memory", "m0", "scc");
     else
@@ -813,9 +808,12 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                                                     unsigned long long *stamps, const PathArgs xa) {
     // Diagnostic build only (-DFA_STAMPS=1, scripts/stamps.py): per-wave s_memtime phase totals.
 #ifdef FA_STAMPS
-    unsigned long long st_t0 = __builtin_amdgcn_s_memtime(), st_rt0 = __builtin_amdgcn_s_memrealtime();
-    unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#define FA_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+    // (32-bit cycle stamps: a block's deltas fit, and half the SGPRs of 64-bit ones keep the
+    // diagnostic build's register pressure near the product's)
+    uint32_t st_t0 = (uint32_t)__builtin_amdgcn_s_memtime();
+    unsigned long long st_rt0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define FA_STAMP(v) const uint32_t v = (uint32_t)__builtin_amdgcn_s_memtime()
 #else
     (void)stamps;
 #define FA_STAMP(v)
@@ -1075,8 +1073,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // pipelined loop: every piece names M0 as an input (hipcc sets it; one wait state in the asm)
     auto stage_pieces = [&](const char *base, const int stride, const int j, const uint32_t m0v, const int *voff) {
         const int key0 = j * kBlockN;
-        dma_tile<NP>(make_quad(base + 2 * (int64_t)key0 * stride, slab_bytes(min(Sk - key0, kBlockN), stride, D)), m0v,
-                     voff);
+        // (make_rsrc_u: the descriptor provably in SGPRs, whatever the register pressure)
+        dma_tile<NP>(make_rsrc_u(base + 2 * (int64_t)key0 * stride, slab_bytes(min(Sk - key0, kBlockN), stride, D)),
+                     m0v, voff);
     };
     auto stage_k = [&](const int j, const int slot) {
         stage_pieces(kb, ks_, j, lds_u32(lds + KV0 + slot * T) + wave * NP * 1024, kvo);
@@ -1223,7 +1222,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     constexpr int G1 = 4 * KS;
     // AD (A-dead tiles, causal diagonal): bit 0 = block A has no visible score in this tile (its S
     // MFMAs are skipped), bit 1 = nor in the previous tile (its late softmax units are skipped)
-    auto phase1 = [&](const char *K, auto PAR, auto SM2, auto DMA, const u32x4 &kq, const u32x4 &vq, auto AD)
+    auto phase1 = [&](const char *K, auto PAR, auto SM2, auto DMA, const rsrc_t &kq, const rsrc_t &vq, auto AD)
         __attribute__((always_inline)) {
         constexpr int c = decltype(PAR)::value, pr = c ^ 1;
         constexpr bool do_sm = decltype(SM2)::value, do_dma = decltype(DMA)::value;
@@ -1235,7 +1234,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             constexpr int g = decltype(G)::value;
             constexpr int ks = g >> 2, i = g & 3, cb = ks & 1;
             // one counted wait per k-step (its two K fragments were read a whole k-step ahead)
+#ifndef FA_EXP_NOLGKM1
             if constexpr (ks > 0 && i == 0) __builtin_amdgcn_s_waitcnt(kLgkm0);
+#endif
             if constexpr (sdead && i < 2) {
             } else {
                 mfma_sq<F, QB + 4 * ((i >> 1) * KS + ks)>(ks == 0, S[c][i], kf[cb][i & 1]);
@@ -1261,8 +1262,14 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                 } else
 #endif
                 {
+#ifdef FA_EXP_NOLGKM1  // (timing experiment, stamps builds only: K reads the compiler cannot see and no
+                       // k-step waits -- how much of phase 1 the per-k-step LDS waits cost; wrong results)
+                    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(kf[cb ^ 1][0]) : "v"(k_addr[ks + 1]), "i"(KV0 + c * T));
+                    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(kf[cb ^ 1][1]) : "v"(k_addr[ks + 1]), "i"(KV0 + c * T + 32 * RB));
+#else
                     kf[cb ^ 1][0] = *(const u32x4 *)(K + k_addr[ks + 1]);
                     kf[cb ^ 1][1] = *(const u32x4 *)(K + 32 * RB + k_addr[ks + 1]);
+#endif
                 }
             }
             if constexpr (do_dma && i == 2) {
@@ -1355,7 +1362,12 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         u32x4 va[2][DTL];
         auto rd = [&](const int kk, const int n, u32x4 *dst) {
             const int rowoff = ((kk >> 1) * 32 + (kk & 1) * 16) * RB + (n & 1) * 8 * RB;
+#ifdef FA_EXP_NOLGKM2  // (timing experiment, as FA_EXP_NOLGKM1 for the V^T reads of phase 2)
+            u32x2 x;
+            asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(x) : "v"(v_addr[n >> 1]), "i"(KV0 + (2 + cp) * T + rowoff));
+#else
             const u32x2 x = tr_read(V + rowoff + v_addr[n >> 1]);
+#endif
             dst[n >> 1][2 * (n & 1)] = x[0];
             dst[n >> 1][2 * (n & 1) + 1] = x[1];
         };
@@ -1367,7 +1379,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             constexpr int X = i / DTL, dt = i % DTL;
             // one counted wait per 16-key step: its V^T fragments were read in the first DTL gaps
             // of the previous step, two per gap
+#ifndef FA_EXP_NOLGKM2
             if constexpr (kk > 0 && i == 0) __builtin_amdgcn_s_waitcnt(kLgkm0);
+#endif
             if constexpr (!(pdead && X == 0)) agpr_mfma<F, X * 16 * DTL + 16 * dt, true>(va[kk & 1][dt], P[cp][4 * X + kk]);
             FA_SCHED_FENCE();  // (see phase 1)
             if constexpr (kk + 1 < 4 && i < DTL) {
@@ -1438,12 +1452,14 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         });
     };
 
-    // pipelined loop: the K_{j+1} / V_j descriptors are SGPR quads advanced in place (no 64-bit
-    // multiply nor descriptor assembly per tile); a full tile spans full_k / full_v bytes, the Sk
-    // tail tile fewer, a tile past Sk none
+    // pipelined loop: running tile pointers (no 64-bit multiply per tile) and descriptor sizes
+    // without branches; a full tile spans full_k / full_v bytes, the Sk tail tile fewer, a tile
+    // past Sk none. (A descriptor carried across tiles as a plain u32x4 and advanced in place
+    // saved its assembly, but hipcc may then keep it in VGPRs, which an asm "s" operand cannot
+    // take: rsrc_t keeps it in SGPRs.)
     const uint32_t full_k = slab_bytes(kBlockN, ks_, D), full_v = slab_bytes(kBlockN, vs_, D);
     const int64_t step_k = 2 * (int64_t)kBlockN * ks_, step_v = 2 * (int64_t)kBlockN * vs_;
-    u32x4 kq, vq;       // K tile j + 1 / V tile j of iteration j
+    const char *kp, *vp;  // K tile j + 1 / V tile j of iteration j
     int kfe = 0;        // tiles below kfe are full (this block's Sk)
     uint32_t k_last = 0;  // the bytes of K tile kfe (the Sk tail, or 0)
     auto tile_bytes = [&](const int key0, const uint32_t full, const int stride) {
@@ -1455,13 +1471,13 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     for (;;) {
     // ---- block prologue: Q and K_0 of this block are in flight ------------------------------
 #ifdef FA_STAMPS
-    st_t0 = __builtin_amdgcn_s_memtime();
+    st_t0 = (uint32_t)__builtin_amdgcn_s_memtime();
     st_rt0 = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
     for (int i = 0; i < 8; ++i) st_acc[i] = 0;
 #endif
-    kq = make_quad(kb + (j_lo + 1) * step_k, 0u);
-    vq = make_quad(vb + j_lo * step_v, 0u);
+    kp = kb + (j_lo + 1) * step_k;
+    vp = vb + j_lo * step_v;
     kfe = Sk / kBlockN;
     k_last = tile_bytes(kfe * kBlockN, full_k, ks_);
     if (rope_q) load_q_rope();
@@ -1538,13 +1554,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             st[0].t = 0.f;
         }
         FA_STAMP(sa);
-        if constexpr (mk == 0) {  // unmasked: j + 1 <= n_pipe <= kfe, V_j full
-            kq[2] = j + 1 < kfe ? full_k : k_last;
-            vq[2] = full_v;
-        } else {
-            kq[2] = tile_bytes((j + 1) * kBlockN, full_k, ks_);
-            vq[2] = tile_bytes(j * kBlockN, full_v, vs_);
-        }
+        // (unmasked: j + 1 <= n_pipe <= kfe, V_j full)
+        const rsrc_t kq = make_rsrc(kp, mk == 0 ? (j + 1 < kfe ? full_k : k_last) : tile_bytes((j + 1) * kBlockN, full_k, ks_));
+        const rsrc_t vq = make_rsrc(vp, mk == 0 ? full_v : tile_bytes(j * kBlockN, full_v, vs_));
         // FA_EXP_*: timing experiments of the stamps build only (results are garbage)
 #if defined(FA_EXP_NOSM)
         phase1(lds + KV0 + c * T, PAR, IC<0>{}, IC<1>{}, kq, vq, AD{});
@@ -1553,8 +1565,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #else
         phase1(lds + KV0 + c * T, PAR, IC<1>{}, IC<1>{}, kq, vq, AD{});
 #endif
-        quad_advance(kq, step_k);
-        quad_advance(vq, step_v);
+        kp += step_k;
+        vp += step_v;
 #ifndef FA_EXP_NOMASK  // (timing experiment of the stamps build only: no mask step, wrong results)
         if constexpr (mk != 0) {  // diagonal / tail tile: mask S before phase 2
             // (per wave and block: only where some score of its 32 rows is hidden; on a causal
@@ -1584,7 +1596,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         FA_STAMP(sd);
         __syncthreads();
 #ifdef FA_STAMPS
-        const unsigned long long se = __builtin_amdgcn_s_memtime();
+        const uint32_t se = (uint32_t)__builtin_amdgcn_s_memtime();
 #ifdef FA_STAMPS_MASKED  // (diagnostic: the tile columns of the record count masked tiles only)
         if constexpr (mk != 0)
 #endif
@@ -1661,7 +1673,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         const char *K = lds + KV0 + sl * T;
         const char *V = lds + KV0 + (2 + sl) * T;
         const int key0 = j * kBlockN;
-        phase1(K, IC<0>{}, IC<0>{}, IC<0>{}, kq, vq, IC<0>{});  // (no DMA: the descriptors are unused)
+        phase1(K, IC<0>{}, IC<0>{}, IC<0>{}, make_rsrc(nullptr, 0u), make_rsrc(nullptr, 0u), IC<0>{});  // (no DMA)
         s_ready(S[0][0], S[0][1]);
         s_ready(S[0][2], S[0][3]);
         mask(S[0][0], S[0][1], mw, key0);
@@ -1757,7 +1769,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #ifdef FA_STAMPS
     {
         __builtin_amdgcn_s_waitcnt(0);
-        const unsigned long long s_end = __builtin_amdgcn_s_memtime(), rt_end = __builtin_amdgcn_s_memrealtime();
+        const uint32_t s_end = (uint32_t)__builtin_amdgcn_s_memtime();
+        const unsigned long long rt_end = __builtin_amdgcn_s_memrealtime();
         if (stamps && lane == 0) {
             // per Q block: [total, p1, p2+rescale, dma wait, barrier, tiles, drain (+ next block's
             //  prefetch issue), prologue, epilogue, realtime (100 MHz ticks), start time, xcc]
