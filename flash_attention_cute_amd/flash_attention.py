@@ -22,6 +22,7 @@ same registrations (CPU default, "cuda" kernel, fake) and the same pad / contigu
 """
 from __future__ import annotations
 
+import os
 import warnings
 from typing import Optional
 
@@ -149,13 +150,30 @@ def flash_attention_varlen_forward_fake(q, k, v, cu_seqlens_q, cu_seqlens_k, max
     return torch.empty_like(q)
 
 
+_CHECK_VARLEN = os.environ.get("FA_CHECK_VARLEN", "0") not in ("", "0")
+
+
+def _check_varlen_maxima(cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k):
+    """Raise if a sequence is longer than the max_seqlen the caller passed (FA_CHECK_VARLEN=1)."""
+    for name, cu, mx in (("q", cu_seqlens_q, max_seqlen_q), ("k", cu_seqlens_k, max_seqlen_k)):
+        longest = int((cu[1:] - cu[:-1]).max()) if cu.numel() > 1 else 0
+        if longest > mx:
+            raise ValueError(f"max_seqlen_{name}={mx} is smaller than the longest sequence ({longest}) "
+                             f"in cu_seqlens_{name}")
+
+
 def flash_attn_varlen_func(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, softmax_scale=None,
                            causal=False, window_left=-1):
     """Attention over packed sequences: q [total_q, Hq, D], k/v [total_k, Hkv, D]; sequence b owns rows
     [cu_seqlens_q[b], cu_seqlens_q[b+1]) of q and [cu_seqlens_k[b], cu_seqlens_k[b+1]) of k/v
-    (int32, on q's device). ``max_seqlen_q`` / ``max_seqlen_k`` must be the true maxima.
+    (int32, on q's device). ``max_seqlen_q`` / ``max_seqlen_k`` must be the true maxima: the GPU grid
+    is sized by ``max_seqlen_q``, so a smaller value leaves the rows of longer sequences uncomputed.
+    With ``FA_CHECK_VARLEN=1`` in the environment both are verified against ``cu_seqlens_*`` (one host
+    sync per call; off by default, as in the reference's varlen API).
     ``window_left >= 0``: the local window of ``flash_attn_window_func`` within each sequence."""
     softmax_scale = (q.size(-1) ** -0.5) if softmax_scale is None else softmax_scale
+    if _CHECK_VARLEN:
+        _check_varlen_maxima(cu_seqlens_q, cu_seqlens_k, int(max_seqlen_q), int(max_seqlen_k))
     return torch.ops.flash_attention.varlen_forward(q, k, v, cu_seqlens_q, cu_seqlens_k, int(max_seqlen_q),
                                                     int(max_seqlen_k), softmax_scale, causal, int(window_left))
 

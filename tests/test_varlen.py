@@ -91,6 +91,22 @@ def test_varlen_op_cpu_default(causal):
     np.testing.assert_allclose(out.double().numpy(), ref, atol=2e-5, rtol=1e-4)
 
 
+def test_varlen_max_seqlen_check(monkeypatch):
+    """FA_CHECK_VARLEN=1: a max_seqlen below the longest sequence raises instead of silently leaving
+    rows uncomputed (off by default: no host sync)."""
+    from flash_attention_cute_amd import flash_attention as fam
+
+    q, k, v, cu_q, cu_k, mq, mk = pack(CASES[1], torch.float32, 5)
+    fam._check_varlen_maxima(cu_q, cu_k, mq, mk)  # true maxima pass
+    with pytest.raises(ValueError, match="max_seqlen_q"):
+        fam._check_varlen_maxima(cu_q, cu_k, mq - 1, mk)
+    with pytest.raises(ValueError, match="max_seqlen_k"):
+        fam._check_varlen_maxima(cu_q, cu_k, mq, mk - 1)
+    monkeypatch.setattr(fam, "_CHECK_VARLEN", True)
+    with pytest.raises(ValueError):
+        fam.flash_attn_varlen_func(q, k, v, cu_q, cu_k, mq - 1, mk)
+
+
 def test_varlen_op_registration():
     import flash_attention_cute_amd  # noqa: F401
 
