@@ -836,12 +836,14 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     constexpr int kNL = 2 * (32 - kV0);  // late exp units of phase 1
     constexpr int QB = 128;  // Q fragments: AGPRs a[QB + 4*(X*KS + ks)] (fa_agpr_asm.inc)
 #ifndef FA_QLDS
-#define FA_QLDS 2
+#define FA_QLDS 1
 #endif
     // Q staging (kQL): 0 = HBM -> AGPR loads issued under the previous block's drain; 1 = LDS-DMA
     // into a Q image (K's swizzle) under the drain, read into the AGPRs at the block prologue;
-    // 2 = the same pieces spread over the previous block's tiles (kQPT per tile, phase 1), so the
-    // block switch moves no Q bytes
+    // 2 = the same pieces spread over the previous block's tiles (kQPT per tile, phase 2), so the
+    // block switch moves no Q bytes. 1 is the default since the round-3 instruction cut: the two
+    // per-tile checks of 2 cost more than the switch's Q burst (A/B +0.4..0.5 % on C2 / C4 / C5,
+    // bit-identical, profiles/r3_ab_q_staging.log; round 2 had measured 2 ahead)
     constexpr int kQL = FA_QLDS;
     constexpr int kQPT = 2;
 #ifndef FA_QPH
