@@ -6,15 +6,21 @@ Metric (BASELINE.json): attn fwd TFLOPS + %MFMA peak at (B,H,S,D) = (4,32,4096,1
 ``flash_attn_func`` (custom op -> C++ host API -> C-ABI -> HIP kernel) over one batch of
 synthetic N(0,1) q, k, v already resident in HBM.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|c5_layer|decode|window|...] [--strong]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|c5_layer|decode|window|...]
+                  [--weak] [--world W --rank R]
 
 Multi-GPU (launched by torch.distributed.run, one process per GPU; attention tiles are independent,
 so there is no data-path collective -- SURVEY.md 8(e)). A gloo process group carries only the
 barrier and the max-over-ranks of the timings.
-  default ("weak"): every rank runs the whole configured workload on its own seeded inputs;
-  --strong        : ONE global problem (batch = --global-batch, default the config's) is split into
-                    (batch, kv-head) units by flash_attention_cute_amd/shard.py and each rank runs
-                    only its units (strided views, no copies); value = global FLOPs / slowest rank.
+  default ("strong"): ONE global problem (batch = --global-batch, default the
+                    config's; C5: global batch 8) is split into (batch, kv-head) units by
+                    flash_attention_cute_amd/shard.py and each rank runs only its units (strided
+                    views, no copies); value = global FLOPs / slowest rank. C2 at N = 8: 128 (b, h)
+                    units -> 16 per GPU. At N = 1 this is the whole configured workload.
+  --weak          : every rank runs the whole configured workload on its own seeded inputs.
+  --world W --rank R (no torch.distributed): THIS process runs exactly rank R's share of a W-way
+                    strong split on one GPU -- the per-GPU work of the N = W run, measured on one
+                    device (``shard_of`` in the line); value = that share's FLOPs / its time.
 c5_layer: a step is one patched ``LlamaAttention.forward`` (Llama-3-8B dims, random weights,
 reference models/rope_attn_fwd.py:66-120 with this repo's fused RoPE) -- value in tokens/s, with the
 bare op and unpatched HF (SDPA) timed beside it in the same run.
@@ -52,10 +58,10 @@ CONFIGS = {
     "c4": dict(workload="C4 GQA fp16 B4 Hq32 Hkv8 S4096 D128 causal", B=4, Hq=32, Hkv=8, Sq=4096,
                Sk=4096, D=128, dtype="fp16", causal=True),
     # C5: Llama-3-8B attention (Hq32 Hkv8 D128), bf16 causal prefill S4096; by default global batch 8
-    # sharded over (batch, kv-head) units -- one batch row per GPU at N=8 (flash_attention_cute_amd/
-    # shard.py, strong scaling); --weak: a B1 replica per GPU
-    "c5": dict(workload="C5 Llama-3-8B attn bf16 causal Hq32 Hkv8 S4096 D128, B1 per replica", B=1, Hq=32, Hkv=8,
-               Sq=4096, Sk=4096, D=128, dtype="bf16", causal=True),
+    # (strong_batch) sharded over (batch, kv-head) units -- one batch row per GPU at N=8
+    # (flash_attention_cute_amd/shard.py, strong scaling); --weak: a B1 replica per GPU
+    "c5": dict(workload="C5 Llama-3-8B attn bf16 causal Hq32 Hkv8 S4096 D128", B=1, Hq=32, Hkv=8,
+               Sq=4096, Sk=4096, D=128, dtype="bf16", causal=True, strong_batch=8),
     # the patched HF attention layer around the op at C5's dims (prefill of S tokens, B per GPU)
     "c5_layer": dict(workload="C5 layer: patched Llama-3-8B LlamaAttention.forward bf16 causal B1(per GPU) S4096 "
                               "(hidden 4096, Hq32 Hkv8 D128, rope_theta 5e5)", B=1, Hq=32, Hkv=8, Sq=4096, Sk=4096,
@@ -244,6 +250,62 @@ def cpu_port(q, k, v, c, target_s: float, cores: int) -> dict:
                       f"{t_port:.2f} s, oracle/fa_oracle.c fp32 OpenMP)"}
 
 
+def run_mode(config_key: str, weak: bool = False, global_batch: int = 0, world: int = 1, rank: int = 0,
+             emu_world: int = 0, emu_rank: int = 0) -> dict:
+    """How this process's timed launches relate to the job.
+
+    strong (default): one global problem of ``global_batch`` rows (default the config's
+    ``strong_batch``, else its B) split over ``split_world`` ranks by shard.plan; this process runs
+    the share of ``split_rank``. ``emu_world`` > 0 runs rank ``emu_rank``'s share of an
+    ``emu_world``-way split in this one process (no torch.distributed). weak: every rank runs the
+    whole configured workload (c5_layer always: a layer call per GPU)."""
+    c = CONFIGS[config_key]
+    emulated = emu_world > 0
+    if emulated and world > 1:
+        raise ValueError("--world/--rank emulate one rank's share in a single process; not under --gpus > 1")
+    strong = not weak and config_key != "c5_layer"
+    if emulated and not strong:
+        raise ValueError("--world/--rank need the strong split (not --weak, not c5_layer)")
+    split_world, split_rank = (emu_world, emu_rank) if emulated else (world, rank)
+    if not 0 <= split_rank < split_world:
+        raise ValueError(f"rank {split_rank} outside world {split_world}")
+    default_gb = c.get("strong_batch", c["B"])
+    gb = (global_batch or default_gb) if strong else c["B"]
+    # the committed PMC pass (profiles/pmc_<config>.json) profiled the default N = 1 run: its traffic
+    # describes these launches only when they are that whole workload
+    whole = (split_world == 1 and gb == default_gb) if strong else default_gb == c["B"]
+    return {"strong": strong, "split_world": split_world, "split_rank": split_rank, "emulated": emulated,
+            "global_batch": gb, "whole_default_workload": whole}
+
+
+def strong_calls(c, q, k, v, runs, dense_fn, window_fn, padded_fn):
+    """One op call per shard.Run of a rank (strided views of the global q [B, Hq, Sq, D] / k, v
+    [B, Hkv, Sk, D], no copies): [(run, call)], and the FLOPs and algorithmic bytes of those calls.
+    Padded configs (``lens``: left padding) pass each run's rows' own key ranges, windowed configs
+    the window."""
+    import torch
+
+    g = c["Hq"] // c["Hkv"]
+    lens_all = c.get("lens")
+    out, fl, by = [], 0.0, 0
+    for r in runs:
+        qv, kv, vv = q[r.b:r.b_end, r.h0 * g:r.h1 * g], k[r.b:r.b_end, r.h0:r.h1], v[r.b:r.b_end, r.h0:r.h1]
+        cr = dict(c, B=r.b_end - r.b, Hq=(r.h1 - r.h0) * g, Hkv=r.h1 - r.h0)
+        if lens_all:
+            cr["lens"] = list(lens_all[r.b:r.b_end])
+            k_end = torch.full((cr["B"],), c["Sk"], dtype=torch.int32, device=q.device)
+            k_start = k_end - torch.tensor(cr["lens"], dtype=torch.int32, device=q.device)
+            call = (lambda a=qv, b_=kv, v_=vv, s=k_start, e=k_end: padded_fn(a, b_, v_, s, e, causal=c["causal"]))
+        elif c.get("W"):
+            call = (lambda a=qv, b_=kv, v_=vv: window_fn(a, b_, v_, c["W"] - 1, causal=c["causal"]))
+        else:
+            call = (lambda a=qv, b_=kv, v_=vv: dense_fn(a, b_, v_, causal=c["causal"]))
+        out.append((r, call))
+        fl += flops(cr)
+        by += algo_bytes(cr)
+    return out, fl, by
+
+
 def load_traffic(config_key: str):
     """(HBM bytes per launch, provenance) from profiles/pmc_<config>.json -- only when that PMC pass
     profiled THIS library (its ``lib_sha16`` equals the loaded library's); otherwise (None, why)."""
@@ -342,17 +404,18 @@ def main() -> None:
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="CPU port sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--strong", action="store_true", help="split one global problem over the ranks (shard.py)")
-    ap.add_argument("--weak", action="store_true", help="c5: every rank runs its own B1 replica instead")
-    ap.add_argument("--global-batch", type=int, default=0, help="--strong: global batch (default: the config's)")
+    ap.add_argument("--strong", action="store_true", help="(the default) split one global problem over the ranks")
+    ap.add_argument("--weak", action="store_true", help="every rank runs the whole configured workload instead")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="strong split: global batch (default: the config's; C5: 8)")
+    ap.add_argument("--world", type=int, default=0,
+                    help="run rank --rank's share of a --world-way strong split in this one process")
+    ap.add_argument("--rank", type=int, default=0, help="see --world")
     ap.add_argument("--warmup-seconds", type=float, default=2.0,
                     help="back-to-back op calls before the W warm-up steps (the clock settles)")
     args = ap.parse_args()
-    if args.config == "c5" and not args.weak:
-        # BASELINE C5 is ONE Llama-3-8B attention problem "batch-sharded across 8xMI355X": global batch 8
-        # split into (batch, kv-head) units over the ranks (strong scaling), also at N = 1
-        args.strong = True
-        args.global_batch = args.global_batch or 8
+    if args.strong and args.weak:
+        ap.error("--strong and --weak exclude each other")
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # not started by torch.distributed.run: start it as a child (never exec) and pass its status on
@@ -384,31 +447,42 @@ def main() -> None:
     dt = torch.float16 if c["dtype"] == "fp16" else torch.bfloat16
     layer = args.config == "c5_layer"
     extra = {}
-    if args.strong:
+    try:
+        mode = run_mode(args.config, weak=args.weak, global_batch=args.global_batch, world=world, rank=rank,
+                        emu_world=args.world, emu_rank=args.rank)
+    except ValueError as e:
+        ap.error(str(e))
+    if mode["strong"]:
         # one global problem, this rank's (batch, kv-head) units (shard.py); same seed on every rank
         from flash_attention_cute_amd import shard
 
-        gb = args.global_batch or c["B"]
-        c = dict(c, B=gb, workload=f"{c['workload']} -> global batch {gb} split over {world} GPU(s)")
+        gb, W, R = mode["global_batch"], mode["split_world"], mode["split_rank"]
+        if W == 1 and gb == c["B"]:
+            c = dict(c, B=gb)
+        elif mode["emulated"]:
+            c = dict(c, B=gb, workload=f"{c['workload']}, global batch {gb}: rank {R}'s share of a {W}-way split")
+        else:
+            c = dict(c, B=gb, workload=f"{c['workload']}, global batch {gb} split over {W} GPU(s)")
         gen = torch.Generator(device=dev).manual_seed(args.seed)
         q = torch.randn(gb, c["Hq"], c["Sq"], c["D"], device=dev, dtype=dt, generator=gen)
         k = torch.randn(gb, c["Hkv"], c["Sk"], c["D"], device=dev, dtype=dt, generator=gen)
         v = torch.randn(gb, c["Hkv"], c["Sk"], c["D"], device=dev, dtype=dt, generator=gen)
-        runs = shard.rank_runs(gb, c["Hkv"], world, rank)
-        g = c["Hq"] // c["Hkv"]
-        views = [(q[r.b:r.b_end, r.h0 * g:r.h1 * g], k[r.b:r.b_end, r.h0:r.h1], v[r.b:r.b_end, r.h0:r.h1])
-                 for r in runs]
-        rank_flops = sum(flops(dict(c, B=r.b_end - r.b, Hq=(r.h1 - r.h0) * g)) for r in runs)
-        rank_bytes = sum(algo_bytes(dict(c, B=r.b_end - r.b, Hq=(r.h1 - r.h0) * g, Hkv=r.h1 - r.h0)) for r in runs)
+        runs = shard.rank_runs(gb, c["Hkv"], W, R)
+        run_calls, rank_flops, rank_bytes = strong_calls(c, q, k, v, runs, flash_attn_func, flash_attn_window_func,
+                                                         flash_attn_padded_func)
 
         def step():
-            if c.get("W"):
-                return [flash_attn_window_func(a, b_, v_, c["W"] - 1, causal=c["causal"]) for a, b_, v_ in views]
-            return [flash_attn_func(a, b_, v_, causal=c["causal"]) for a, b_, v_ in views]
+            return [f() for _, f in run_calls]
 
-        extra["shard"] = {"units": f"{c['B'] * c['Hkv']} (batch, kv-head)", "rank0_runs": len(runs)}
+        extra["shard"] = {"units": f"{c['B'] * c['Hkv']} (batch, kv-head)", "world": W, "rank": R,
+                          "rank_runs": len(runs), "rank_units": sum((r.b_end - r.b) * (r.h1 - r.h0) for r in runs)}
+        if mode["emulated"]:
+            extra["shard_of"] = {"world": W, "rank": R, "global_flops": flops(c), "rank_flops": rank_flops,
+                                 "note": "one rank's share of the W-way strong split, run alone on this GPU"}
     else:
-        gen = torch.Generator(device=dev).manual_seed(args.seed + rank)  # per-rank shard of batch x heads
+        if world > 1 or c.get("strong_batch", c["B"]) != c["B"]:
+            c = dict(c, workload=f"{c['workload']}, B{c['B']} replica per GPU")
+        gen = torch.Generator(device=dev).manual_seed(args.seed + rank)  # per-rank replica
         q = torch.randn(c["B"], c["Hq"], c["Sq"], c["D"], device=dev, dtype=dt, generator=gen)
         k = torch.randn(c["B"], c["Hkv"], c["Sk"], c["D"], device=dev, dtype=dt, generator=gen)
         v = torch.randn(c["B"], c["Hkv"], c["Sk"], c["D"], device=dev, dtype=dt, generator=gen)
@@ -486,11 +560,13 @@ def main() -> None:
         extra["layer"]["hf_sdpa_tokens_per_s"] = round(c["B"] * c["Sq"] / (extra["layer"]["hf_sdpa_layer_ms"] * 1e-3), 1)
         extra["layer"]["layer_TFLOPS"] = round((extra["layer"]["projection_flops"] + extra["layer"]["attention_flops"])
                                                / (elapsed / args.steps) / 1e12, 2)
-    elif args.strong:
+    elif mode["emulated"]:  # the one GPU's share, timed alone
+        value, unit = rank_flops * args.steps / elapsed / 1e12, "TFLOPS"
+    elif mode["strong"]:
         value, unit = flops(c) * args.steps / elapsed / 1e12, "TFLOPS"
     else:
         value, unit = n_gpus * flops(c) * args.steps / elapsed / 1e12, "TFLOPS"
-    tf_per_gpu = (flops(c) / n_gpus if args.strong else flops(c)) * args.steps / elapsed / 1e12
+    tf_per_gpu = value / n_gpus
     result = {
         "metric": metric_of(args.config, c),
         "value": round(value, 3),
@@ -501,26 +577,31 @@ def main() -> None:
         "device_warmup_s": args.warmup_seconds,
         "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
         "higher_is_better": True,
-        "scaling": "strong" if args.strong else "weak",
+        "scaling": "strong" if mode["strong"] else "weak",
         "vs_baseline": None,
         "dtype": c["dtype"],
-        "data": ("synthetic N(0,1) q/k/v, one global seed, sharded by (batch, kv-head)" if args.strong else
+        "data": ("synthetic N(0,1) q/k/v, one global seed, sharded by (batch, kv-head)" if mode["strong"] else
                  "synthetic N(0,1) q/k/v, seed + rank, resident in HBM") +
                 ("; random-init Llama-3-8B attention weights, no checkpoint" if layer else ""),
         "config": {"workload": c["workload"], "batch": c["B"], "heads_q": c["Hq"], "heads_kv": c["Hkv"],
                    "seqlen_q": c["Sq"], "seqlen_kv": c["Sk"], "headdim": c["D"], "causal": c["causal"],
                    **({"window": c["W"]} if c.get("W") else {}),
-                   "parallelism": (f"dp{n_gpus}: (batch, kv-head) units of one problem split over ranks, no collective"
-                                   if args.strong else
-                                   f"dp{n_gpus} (independent batch x head shard per GPU, no collective)")},
+                   "parallelism": (f"one rank of dp{mode['split_world']} (its (batch, kv-head) units, run alone)"
+                                   if mode["emulated"] else
+                                   f"dp{n_gpus}: (batch, kv-head) units of one problem split over ranks, no collective"
+                                   if mode["strong"] else
+                                   f"dp{n_gpus} (independent replica of the workload per GPU, no collective)")},
         "pct_mfma_peak": None if layer else round(100.0 * tf_per_gpu / PEAK_TFLOPS, 2),
-        # rank 0's kernel: its FLOPs / bytes over the mean HIP-event time of its launches
-        "roofline": roofline(c, kern_ms, load_traffic(args.config) if not args.strong else None,
+        # rank 0's kernel: its FLOPs / bytes over the mean HIP-event time of its launches; the PMC
+        # traffic only when these launches are the profiled (default N = 1) workload
+        "roofline": roofline(c, kern_ms, load_traffic(args.config) if mode["whole_default_workload"] else
+                             (None, {"traffic_source": None, "traffic_note": "launches differ from the profiled "
+                                     "workload (a shard or another batch)"}),
                              rank_flops=rank_flops, rank_bytes=rank_bytes),
         "cpu_baseline": None,
         **extra,
     }
-    if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
+    if rank == 0 and n_gpus == 1 and not mode["emulated"] and not args.no_cpu_baseline:
         result["cpu_baseline"] = (cpu_layer_baseline(c, args.seed) if layer else
                                   cpu_baseline(q, k, v, c, args.cpu_seconds))
     if rank == 0:
