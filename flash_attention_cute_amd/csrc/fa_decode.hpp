@@ -83,10 +83,12 @@ __global__ __launch_bounds__(256, 1) void fa_decode(const fa_fwd_params p, const
     const float thr_raw = kRescaleThr / sc;
     // this batch row's keys: positions [k0, k0 + Sk) (a padded batch's key range, DecArgs); else
     // every key
+    // (clamped to [0, seqlen_kv]: out-of-range positions never address outside the K / V rows)
     int k0 = 0, Sk = (int)p.seqlen_kv;
     if (a.k_lo) {
-        k0 = a.k_lo[b];
-        Sk = max(a.k_hi[b] - k0, 0);
+        const int sk_all = Sk;
+        k0 = min(max(a.k_lo[b], 0), sk_all);
+        Sk = min(max(a.k_hi[b], k0), sk_all) - k0;
     }
     const int diag = Sk - Sq;
 

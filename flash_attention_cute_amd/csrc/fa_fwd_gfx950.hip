@@ -260,10 +260,14 @@ __global__ void padded_rows(int32_t *q_rng, int32_t *k_rng, const int32_t *qs, c
                             const int32_t *ke, int batch, int64_t q_rpb, int64_t k_rpb, int sq, int sk) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b < batch) {
-        q_rng[b] = (int32_t)(b * q_rpb + (qs ? qs[b] : 0));
-        q_rng[batch + b] = (int32_t)(b * q_rpb + (qe ? qe[b] : sq));
-        k_rng[b] = (int32_t)(b * k_rpb + (ks ? ks[b] : 0));
-        k_rng[batch + b] = (int32_t)(b * k_rpb + (ke ? ke[b] : sk));
+        // positions clamped to the dimension (start into [0, n], end into [start, n]): a range past
+        // the tensor never addresses another batch row's rows or memory past the allocation
+        const int q0 = qs ? min(max(qs[b], 0), sq) : 0, q1 = qe ? min(max(qe[b], q0), sq) : sq;
+        const int k0 = ks ? min(max(ks[b], 0), sk) : 0, k1 = ke ? min(max(ke[b], k0), sk) : sk;
+        q_rng[b] = (int32_t)(b * q_rpb + q0);
+        q_rng[batch + b] = (int32_t)(b * q_rpb + q1);
+        k_rng[b] = (int32_t)(b * k_rpb + k0);
+        k_rng[batch + b] = (int32_t)(b * k_rpb + k1);
     }
 }
 

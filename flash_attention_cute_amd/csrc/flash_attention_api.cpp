@@ -498,9 +498,16 @@ torch::Tensor flash_attention_padded_fwd(torch::Tensor &q, torch::Tensor &k, tor
         qx = qx.reshape({bs, head_q, seqlen_q, headdim});
         if (!aligned16(qx)) qx = qx.contiguous();
     }
-    if (!pack && rows_per_batch(qx) < 0) qx = qx.contiguous();  // (the prefill path may run)
+    if (rows_per_batch(qx) < 0) qx = qx.contiguous();  // (the prefill path may run, also after a pack)
     auto o = torch::empty_like(qx);
     if (!aligned16(o) || o.strides() != qx.strides()) o = torch::empty(qx.sizes(), qx.options());
+    // the prefill kernel addresses q and o rows with ONE rows-per-batch multiple: a q that is not
+    // dense (a seqlen slice of a longer buffer, a view cut from a wider tensor) leaves empty_like with
+    // a contiguous o, so q is made contiguous too
+    if (rows_per_batch(o) != rows_per_batch(qx)) {
+        qx = qx.contiguous();
+        o = torch::empty(qx.sizes(), qx.options());
+    }
     if (q_ranges) o.zero_();  // rows outside the query ranges are not written by the kernel
 
     fa_padded_params pp;

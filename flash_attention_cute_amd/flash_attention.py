@@ -150,7 +150,9 @@ def flash_attention_varlen_forward_fake(q, k, v, cu_seqlens_q, cu_seqlens_k, max
     return torch.empty_like(q)
 
 
-_CHECK_VARLEN = os.environ.get("FA_CHECK_VARLEN", "0") not in ("", "0")
+def _check_varlen_enabled() -> bool:
+    """FA_CHECK_VARLEN, read at every call (setting it after import takes effect)."""
+    return os.environ.get("FA_CHECK_VARLEN", "0") not in ("", "0")
 
 
 def _check_varlen_maxima(cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k):
@@ -168,11 +170,11 @@ def flash_attn_varlen_func(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, ma
     [cu_seqlens_q[b], cu_seqlens_q[b+1]) of q and [cu_seqlens_k[b], cu_seqlens_k[b+1]) of k/v
     (int32, on q's device). ``max_seqlen_q`` / ``max_seqlen_k`` must be the true maxima: the GPU grid
     is sized by ``max_seqlen_q``, so a smaller value leaves the rows of longer sequences uncomputed.
-    With ``FA_CHECK_VARLEN=1`` in the environment both are verified against ``cu_seqlens_*`` (one host
-    sync per call; off by default, as in the reference's varlen API).
+    With ``FA_CHECK_VARLEN=1`` in the environment (read at every call) both are verified against
+    ``cu_seqlens_*`` (one host sync per call; off by default, as in the reference's varlen API).
     ``window_left >= 0``: the local window of ``flash_attn_window_func`` within each sequence."""
     softmax_scale = (q.size(-1) ** -0.5) if softmax_scale is None else softmax_scale
-    if _CHECK_VARLEN:
+    if _check_varlen_enabled():
         _check_varlen_maxima(cu_seqlens_q, cu_seqlens_k, int(max_seqlen_q), int(max_seqlen_k))
     return torch.ops.flash_attention.varlen_forward(q, k, v, cu_seqlens_q, cu_seqlens_k, int(max_seqlen_q),
                                                     int(max_seqlen_k), softmax_scale, causal, int(window_left))

@@ -23,7 +23,7 @@ csrc/flash_attention_api.cpp), ``attn.transpose(1, 2).reshape(B, S, -1)`` is cop
 """
 from __future__ import annotations
 
-from typing import Optional, Tuple
+from typing import NamedTuple, Optional, Tuple
 
 import torch
 from torch import nn
@@ -37,12 +37,40 @@ from .flash_attention import (_bottom_right_causal, _window_mask, apply_rope, fl
 # (A/B measurements, scripts/benchmark_llm.py --no-fused-rope).
 FUSE_ROPE = True
 
-# Attention masks are validated on the host by default (a mask this lowering cannot express raises
-# instead of being ignored), which costs host synchronisations. True TRUSTS the mask to be causal +
-# key padding with each sequence's real tokens one contiguous run (left or right padding, what
-# ``generate`` builds): the padded path then runs without any host synchronisation, so a decode
-# step can be captured in a HIP graph.
+# How an HF attention mask is lowered (``lower_mask``: every check computed on the device):
+#  * eager calls read the checks back with ONE host synchronisation per call and take the exact
+#    path -- the dense kernels when the mask hides nothing beyond causal / window, the padded kernel
+#    in place when each sequence's real tokens are one run, the packed varlen kernel for other
+#    padding, NotImplementedError for masks none of them expresses;
+#  * under HIP-graph capture (torch.cuda.is_current_stream_capturing()) nothing is read back: the
+#    padded kernel always runs, and a batch row whose mask it cannot express gets an empty range
+#    (output 0) and is counted in a device-side error counter (``mask_errors()`` reads it);
+#  * TRUST_PADDING_MASK = True skips the checks altogether (no synchronisation in eager calls
+#    either): the mask is trusted to be causal + key padding with one real-token run per sequence
+#    (left or right padding, what ``generate`` builds).
 TRUST_PADDING_MASK = False
+
+_MASK_ERRORS = {}  # device -> int32 [1] count of batch rows whose mask the padded kernel could not express
+
+
+def mask_errors(device=None, reset: bool = False) -> int:
+    """Batch rows (summed over calls) whose attention mask was not expressible while lowering without
+    a host synchronisation (graph capture); their outputs were zeroed. One host synchronisation."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    t = _MASK_ERRORS.get(dev)
+    if t is None:
+        return 0
+    n = int(t.item())
+    if reset:
+        t.zero_()
+    return n
+
+
+def _error_counter(dev: torch.device) -> torch.Tensor:
+    t = _MASK_ERRORS.get(dev)
+    if t is None:  # (created by the first eager call, ahead of a capture's warm-up)
+        t = _MASK_ERRORS[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
+    return t
 
 
 def rotate_half(x: torch.Tensor) -> torch.Tensor:
@@ -61,69 +89,128 @@ def apply_rotary_pos_emb(q, k, cos, sin, position_ids=None, unsqueeze_dim=1):
     return q * cos + rotate_half(q) * sin, k * cos + rotate_half(k) * sin
 
 
-def key_padding(attention_mask: Optional[torch.Tensor], sq: int, sk: int, causal: bool,
-                window_left: Optional[int] = None) -> Optional[torch.Tensor]:
-    """Lower an HF attention mask to per-token validity ``[B, Sk]`` (True = real token), or None when it
-    masks nothing beyond the plain causal (and, with ``window_left``, sliding-window) mask.
+class Lowering(NamedTuple):
+    """An HF attention mask lowered to per-sequence ranges (all device tensors; ``lower_mask``)."""
 
-    Accepted: a 2-D padding mask ``[B, Sk]`` (1 = real token), or the 4-D mask HF builds for SDPA /
-    eager ``[B, 1, Sq, Sk]`` (bool, True = attend; or additive float, 0 = attend) that is exactly
-    "causal (bottom-right) AND inside the window AND key not padding" on every real query row. A
-    query row is real iff its own token (key position m + Sk - Sq) is. Any other mask (chunked /
-    custom) raises NotImplementedError instead of being silently ignored as in the reference
-    (models/rope_attn_fwd.py:40-64 drops ``attention_mask``).
+    kv_valid: torch.Tensor  # [B, Sk] bool: keys some real query row attends
+    q_valid: torch.Tensor   # [B, Sq] bool: query rows whose own token is real
+    k_start: torch.Tensor   # [B] int32: the real keys are positions [k_start, k_end) ...
+    k_end: torch.Tensor
+    q_start: torch.Tensor   # ... the real query rows [q_start, q_end)
+    q_end: torch.Tensor
+    shape_ok: torch.Tensor  # [B] bool: on every real query row the mask is "causal / window AND key real"
+    run_ok: torch.Tensor    # [B] bool: real keys and real query rows each one run, the last real query's
+                            # own key the last real key (the kernels' bottom-right alignment)
+    dense: torch.Tensor     # [] bool: every range is the whole dimension (nothing hidden beyond the shape)
+
+
+def _first_last_count(valid: torch.Tensor):
+    n = valid.shape[1]
+    idx = torch.arange(n, device=valid.device)[None]
+    first = torch.where(valid, idx, n).amin(1)
+    last = torch.where(valid, idx, -1).amax(1)
+    return first, last, valid.sum(1)
+
+
+def lower_mask(attention_mask: Optional[torch.Tensor], sq: int, sk: int, causal: bool,
+               window_left: Optional[int] = None) -> Optional[Lowering]:
+    """Lower an HF attention mask to per-sequence query / key ranges, computed on the device with no
+    host synchronisation (None: no mask).
+
+    Accepted: a 2-D padding mask ``[B, Sk]`` (1 = real token; the queries are the last Sq keys, a
+    dynamic cache), or the 4-D mask HF builds for SDPA / eager ``[B, 1, Sq, Sk]`` (bool, True =
+    attend; or additive float, 0 = attend). With a causal 4-D mask each query row's own key position
+    is read from the mask itself -- the last key a real row attends is its own token -- so the queries
+    may sit anywhere in the keys: the last Sq of a dynamic cache, or mid-way through a static cache
+    whose later slots are empty (the mask hides them). Padding query rows attend no key (left
+    padding) or sit after the real rows (right padding). ``shape_ok`` holds where the mask is exactly
+    "causal (up to the row's own key) AND inside the window AND key real" on every real row; anything
+    else (chunked / document / custom masks) is for the caller to reject instead of being silently
+    dropped as in the reference (models/rope_attn_fwd.py:40-64 ignores ``attention_mask``).
     """
     if attention_mask is None:
         return None
-    if TRUST_PADDING_MASK:  # no validation, no host synchronisation
-        m = attention_mask
-        if m.dim() == 4:
-            return (m[:, 0] if m.dtype == torch.bool else (m[:, 0] == 0)).any(dim=1)
-        return m.bool()
+    m = attention_mask
     if sq > sk:
         raise NotImplementedError("flash_attention_cute_amd: attention_mask with more queries than keys")
-    m = attention_mask
+    dev = m.device
+    ar_q = torch.arange(sq, device=dev)
+    n_ = torch.arange(sk, device=dev)
     if m.dim() == 2:
         if tuple(m.shape[1:]) != (sk,):
             raise NotImplementedError(f"flash_attention_cute_amd: 2-D attention_mask of shape {tuple(m.shape)} "
                                       f"does not cover the {sk} keys")
         kv_valid = m.bool()
+        qpos = (ar_q + (sk - sq))[None]  # [1, Sq]
+        q_valid = kv_valid[:, qpos[0]]
+        shape_ok = torch.ones(m.shape[0], dtype=torch.bool, device=dev)
     elif m.dim() == 4:
         if m.shape[1] != 1 or m.shape[2] != sq or m.shape[3] != sk:
             raise NotImplementedError(f"flash_attention_cute_amd: 4-D attention_mask of shape {tuple(m.shape)} "
                                       f"(expected [B, 1, {sq}, {sk}])")
-        m = m[:, 0] if m.dtype == torch.bool else (m[:, 0] == 0)
-        if window_left is not None:
-            shape = _window_mask(sq, sk, window_left, causal, m.device)
-        elif causal:
-            shape = _bottom_right_causal(sq, sk, m.device)
-        else:
-            shape = torch.ones(sq, sk, dtype=torch.bool, device=m.device)
-        # a key no row attends to is padding; the keys the causal / window shape hides from every row
-        # (the window's prefix) cannot be told apart and are dropped with it: no row sees them
-        kv_valid = m.any(dim=1)
-        allowed = kv_valid[:, None, :] & shape[None]
-        q_valid = kv_valid[:, sk - sq:]
-        if bool(((m != allowed) & q_valid[:, :, None]).any()):
-            raise NotImplementedError("flash_attention_cute_amd: only causal + key-padding attention masks are "
-                                      "supported (this mask masks other scores)")
-        if bool((kv_valid | ~shape.any(dim=0)[None]).all()):
-            return None  # no padding: the shape alone (the dense causal / window kernels)
+        a = m[:, 0] if m.dtype == torch.bool else (m[:, 0] == 0)
+        own = torch.where(a, n_[None, None], -1).amax(2)  # [B, Sq] the last key each row attends
+        if causal:
+            # real rows: own key = offset + row; padding rows attend only earlier keys (right padding,
+            # holes) or none (left padding), so the offset is the largest own - row
+            rel = torch.where(own >= 0, own - ar_q[None], -1 - sk)
+            off = rel.amax(1)
+            q_valid = (own >= 0) & (rel == off[:, None])
+            qpos = off[:, None] + ar_q[None]  # [B, Sq]
+        else:  # (a decode row, Sq == 1, no query range: computed whatever its position; real iff it
+            # attends a key)
+            q_valid = own >= 0
+            qpos = own
+        kv_valid = (a & q_valid[:, :, None]).any(1)
+        shape = torch.ones(1, 1, sk, dtype=torch.bool, device=dev)
+        if causal:
+            shape = shape & (n_[None, None] <= qpos[:, :, None])
+            if window_left is not None:
+                shape = shape & (n_[None, None] >= qpos[:, :, None] - window_left)
+        allowed = kv_valid[:, None, :] & shape
+        # (rows that do not attend their own key are padding: their output is discarded)
+        shape_ok = ~((a != allowed) & q_valid[:, :, None]).any(2).any(1)
     else:
         raise NotImplementedError(f"flash_attention_cute_amd: attention_mask with {m.dim()} dims")
-    if bool(kv_valid.all()):
+    k_first, k_last, k_cnt = _first_last_count(kv_valid)
+    q_first, q_last, q_cnt = _first_last_count(q_valid)
+    k_start = torch.where(k_cnt > 0, k_first, 0)
+    k_end = k_start + k_cnt
+    q_start = torch.where(q_cnt > 0, q_first, 0)
+    q_end = q_start + q_cnt
+    run_ok = ((k_last - k_first + 1 == k_cnt) | (k_cnt == 0)) & ((q_last - q_first + 1 == q_cnt) | (q_cnt == 0))
+    if causal:  # the kernels' bottom-right alignment: the last real query's own key is the last real key
+        last_own = qpos.expand(q_end.shape[0], sq).gather(1, (q_end - 1).clamp(min=0)[:, None])[:, 0]
+        run_ok = run_ok & ((q_cnt == 0) | (k_end == last_own + 1))
+    dense = ((k_start == 0) & (k_end == sk) & (q_start == 0) & (q_end == sq)).all()
+    i32 = lambda t: t.to(torch.int32)  # noqa: E731
+    return Lowering(kv_valid, q_valid, i32(k_start), i32(k_end), i32(q_start), i32(q_end), shape_ok, run_ok, dense)
+
+
+def key_padding(attention_mask: Optional[torch.Tensor], sq: int, sk: int, causal: bool,
+                window_left: Optional[int] = None) -> Optional[torch.Tensor]:
+    """Per-token validity ``[B, Sk]`` (True = real token) of an HF attention mask, or None when it
+    masks nothing beyond the plain causal (and, with ``window_left``, sliding-window) shape; masks the
+    kernels cannot express raise NotImplementedError. ``lower_mask`` plus one host synchronisation."""
+    low = lower_mask(attention_mask, sq, sk, causal, window_left)
+    if low is None:
         return None
-    if window_left is not None:
+    if TRUST_PADDING_MASK:
+        return low.kv_valid
+    shape_ok, run_ok, dense = torch.stack([low.shape_ok.all(), low.run_ok.all(), low.dense]).tolist()
+    _raise_unexpressible(shape_ok, run_ok, window_left)
+    return None if dense else low.kv_valid
+
+
+def _raise_unexpressible(shape_ok: bool, run_ok: bool, window_left: Optional[int]) -> None:
+    if not shape_ok:
+        raise NotImplementedError("flash_attention_cute_amd: only causal + key-padding attention masks are "
+                                  "supported (this mask masks other scores)")
+    if not run_ok and window_left is not None:
         # HF places the window on cache indices, the varlen kernel on the packed real tokens: the two
-        # agree when each sequence's real tokens are one contiguous run (left or right padding)
-        cnt = kv_valid.sum(1)
-        idx = torch.arange(sk, device=kv_valid.device)[None]
-        first = torch.where(kv_valid, idx, sk).amin(1)
-        last = torch.where(kv_valid, idx, -1).amax(1)
-        if bool(((last - first + 1 != cnt) & (cnt > 0)).any()):
-            raise NotImplementedError("flash_attention_cute_amd: a sliding window over padding that is not one "
-                                      "contiguous run per sequence")
-    return kv_valid
+        # agree only when each sequence's real tokens are one contiguous run (left or right padding)
+        raise NotImplementedError("flash_attention_cute_amd: a sliding window over padding that is not one "
+                                  "contiguous run per sequence")
 
 
 def padding_ranges(kv_valid: torch.Tensor, sq: int, check: bool = True):
@@ -158,12 +245,12 @@ def _padded_attention(query, key, value, ranges, causal, scaling, window_left=-1
     return o.transpose(1, 2)
 
 
-def _varlen_attention(query, key, value, kv_valid, causal, scaling, window_left=-1):
+def _varlen_attention(query, key, value, kv_valid, q_valid, causal, scaling, window_left=-1):
     """Padded batch -> packed sequences -> ``flash_attn_varlen_func`` -> padded [B, Sq, Hq, D] (padding
-    rows 0). q/k/v are [B, H, S, D] views; the valid query rows are the last Sq token positions."""
+    rows 0). q/k/v are [B, H, S, D] views. Every sequence's real query rows are the last of its real
+    keys (``lower_mask``'s alignment), so the packed bottom-right causal mask is the original one."""
     b, hq, sq, d = query.shape
     hkv, sk = key.shape[1], key.shape[2]
-    q_valid = kv_valid[:, sk - sq:]
     lens_q = q_valid.sum(1, dtype=torch.int32)
     lens_k = kv_valid.sum(1, dtype=torch.int32)
     cu_q = torch.nn.functional.pad(torch.cumsum(lens_q, 0, dtype=torch.int32), (1, 0))
@@ -180,16 +267,21 @@ def _varlen_attention(query, key, value, kv_valid, causal, scaling, window_left=
     return out.view(b, sq, hq, d)
 
 
+def _capturing(t: torch.Tensor) -> bool:
+    return t.is_cuda and torch.cuda.is_current_stream_capturing()
+
+
 def _flash_attention_forward(module: nn.Module, query: torch.Tensor, key: torch.Tensor, value: torch.Tensor,
                              attention_mask: Optional[torch.Tensor], dropout: float = 0.0,
                              scaling: Optional[float] = None, sliding_window: Optional[int] = None,
                              softcap: Optional[float] = None, **kwargs) -> Tuple[torch.Tensor, None]:
     """Attention core (reference models/rope_attn_fwd.py:40-64): returns [B, Sq, Hq, D], None.
 
-    Unlike the reference, ``attention_mask`` is honoured: a padding mask whose real tokens form one
-    run per sequence (left / right padding) runs the padded kernel on the tensors in place
-    (``padding_ranges``); other padding is packed for the varlen kernel (``key_padding``); masks it
-    cannot express raise."""
+    Unlike the reference, ``attention_mask`` is honoured (``lower_mask``): a mask that hides nothing
+    beyond causal / window runs the dense kernels; one real-token run per sequence (left / right
+    padding, a static cache's empty slots) runs the padded kernel on the tensors in place; other
+    padding is packed for the varlen kernel; masks none of them expresses raise. Under HIP-graph
+    capture the padded kernel always runs and nothing is read back (module header)."""
     kwargs.pop("is_causal", None)
     if softcap is not None:
         raise NotImplementedError("flash_attention_cute_amd: attention logit softcapping is not supported")
@@ -200,16 +292,33 @@ def _flash_attention_forward(module: nn.Module, query: torch.Tensor, key: torch.
     # a sliding window of W keys (transformers: key n visible to the query at position p iff
     # p - W < n <= p) that cuts the visible keys: the local-window kernel, window_left = W - 1
     window_left = sliding_window - 1 if sliding_window is not None and sk > sliding_window else None
+    wl = -1 if window_left is None else window_left
     rope = kwargs.pop("rope_q", None)  # (cos, sin): q still to be rotated (fused path)
-    kv_valid = key_padding(attention_mask, sq, sk, causal, window_left)
-    if kv_valid is not None:
-        if rope is not None:
-            query = apply_rope(query, *rope)
-        wl = -1 if window_left is None else window_left
-        ranges = padding_ranges(kv_valid, sq, check=not TRUST_PADDING_MASK)
-        if ranges is not None:
-            return _padded_attention(query, key, value, ranges, causal, scaling, wl), None
-        return _varlen_attention(query, key, value, kv_valid, causal, scaling, wl), None
+    kwargs.pop("cache_position", None)
+    low = lower_mask(attention_mask, sq, sk, causal, window_left)
+    if low is not None:
+        ranges = (low.k_start, low.k_end, low.q_start, low.q_end)
+        path = "padded"
+        if TRUST_PADDING_MASK:
+            pass
+        elif _capturing(query):
+            # no host read-back: rows the padded kernel cannot express get empty ranges and are counted
+            ok = low.shape_ok & low.run_ok
+            _error_counter(query.device).add_((~ok).sum(dtype=torch.int32))
+            ranges = (low.k_start, torch.where(ok, low.k_end, low.k_start), low.q_start,
+                      torch.where(ok, low.q_end, low.q_start))
+        else:
+            if query.is_cuda:
+                _error_counter(query.device)
+            shape_ok, run_ok, dense = torch.stack([low.shape_ok.all(), low.run_ok.all(), low.dense]).tolist()
+            _raise_unexpressible(shape_ok, run_ok, window_left)
+            path = "dense" if dense else "padded" if run_ok else "varlen"
+        if path != "dense":
+            if rope is not None:
+                query = apply_rope(query, *rope)
+            if path == "padded":
+                return _padded_attention(query, key, value, ranges, causal, scaling, wl), None
+            return _varlen_attention(query, key, value, low.kv_valid, low.q_valid, causal, scaling, wl), None
     if window_left is not None:
         if rope is not None:
             query = apply_rope(query, *rope)

@@ -184,7 +184,9 @@ int fa_fwd_gfx950_varlen_check(const fa_varlen_params *params, int dtype, int ca
  * fa_fwd_gfx950 (seqlen_q / seqlen_kv = the padded lengths). Batch row b's real keys are positions
  * [k_start[b], k_end[b]) of its Sk and its real queries positions [q_start[b], q_end[b]) of its Sq --
  * int32 arrays of B entries in DEVICE memory; q_start == q_end == NULL means every query row,
- * k_start == k_end == NULL every key. Masks are bottom-right aligned per sequence (key n of the
+ * k_start == k_end == NULL every key. The kernels clamp every range to its dimension (start into
+ * [0, Sq] / [0, Sk], end into [start, Sq] / [start, Sk]) on the device, so an out-of-range position
+ * never reads or writes outside the tensors. Masks are bottom-right aligned per sequence (key n of the
  * range visible to query m of the range iff n - k_start <= m - q_start + Sk_b - Sq_b);
  * window_left >= 0 adds the local window of fa_fwd_gfx950_window per sequence (< 0: none). Output
  * rows outside the query ranges are NOT written (the torch binding zero-fills them first); rows with

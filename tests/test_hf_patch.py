@@ -391,3 +391,160 @@ def test_patch_sliding_window_layer_matches_hf_on_gpu(device, dtype):
     got = run_window_layer(cfg, device, dtype, seqs, 128, patch=True)
     tol = 2e-2 if dtype == torch.bfloat16 else 4e-3
     torch.testing.assert_close(got.float(), ref, atol=tol, rtol=0)
+
+
+# ---- masks lowered on the device: static caches, graph capture ----------
+def _generate_tokens(model, ids, mask, patch, **kw):
+    with torch.no_grad(), warnings.catch_warnings(), (patched(ml.LlamaAttention) if patch else _null()):
+        warnings.simplefilter("ignore")
+        return model.generate(ids, attention_mask=mask, do_sample=False, pad_token_id=0, **kw)
+
+
+@pytest.mark.parametrize("cache", ["dynamic", "static"])
+def test_patched_generate_with_left_padding_matches_hf_on_cpu(cache):
+    """Left-padded greedy generate through a DynamicCache and a StaticCache (whose keys past the current
+    position are empty slots the 4-D mask hides: the query rows sit mid-way through the keys) gives the
+    token ids of unpatched transformers."""
+    cfg = tiny_llama(hq=4, hkv=2, d=32)
+    torch.manual_seed(0)
+    model = transformers.LlamaForCausalLM(cfg).eval()
+    ids = torch.randint(1, cfg.vocab_size, (3, 12))
+    mask = torch.ones_like(ids)
+    mask[1, :5] = 0
+    mask[2, :11] = 0
+    ids[mask == 0] = 0
+    kw = dict(max_new_tokens=6, cache_implementation=cache)
+    assert torch.equal(_generate_tokens(model, ids, mask, True, **kw), _generate_tokens(model, ids, mask, False, **kw))
+
+
+def _static_masks(valid, pos, s, total):
+    """HF's 4-D SDPA mask of s new tokens at positions pos.. over a static cache of ``total`` slots."""
+    p_ = torch.arange(pos, pos + s)[:, None]
+    n = torch.arange(total)[None, :]
+    return ((n <= p_)[None] & valid[:, None, :total])[:, None]
+
+
+def test_lower_mask_static_cache_and_padding_kinds():
+    from flash_attention_cute_amd.hf_attention import lower_mask
+
+    total = 10
+    valid = torch.zeros(3, total, dtype=torch.bool)
+    valid[0, :7] = True          # no padding, 7 tokens so far
+    valid[1, 3:7] = True         # left padding
+    valid[2, :7] = True
+    valid[2, 4] = False          # a hole
+    low = lower_mask(_static_masks(valid, 0, 7, total)[:, :, :7], 7, total, True)  # prefill rows 0..6
+    # (row 2: six real tokens, not one run -- its ranges are not used, the varlen path packs it)
+    assert low.k_start.tolist() == [0, 3, 0] and low.k_end.tolist() == [7, 7, 6]
+    assert low.q_start.tolist() == [0, 3, 0] and low.q_end.tolist() == [7, 7, 6]
+    assert low.shape_ok.tolist() == [True, True, True] and low.run_ok.tolist() == [True, True, False]
+    assert not bool(low.dense)  # the static cache's empty slots are hidden: not the dense kernel
+    dec = lower_mask(_static_masks(valid, 6, 1, total), 1, total, False)  # decode at position 6
+    assert dec.k_start.tolist() == [0, 3, 0] and dec.k_end.tolist() == [7, 7, 6]
+    assert dec.run_ok.tolist() == [True, True, False]
+    # a document (block-diagonal) mask is not causal + padding
+    doc = _static_masks(torch.ones(1, total, dtype=torch.bool), 0, 7, total)[:, :, :7].clone()
+    doc[0, 0, 4:, :4] = False
+    assert lower_mask(doc, 7, total, True).shape_ok.tolist() == [False]
+
+
+class _NoHostReads:
+    """Any read-back of a tensor value on the host (item / tolist / bool / int) raises."""
+
+    NAMES = ("item", "tolist", "__bool__", "__int__", "__index__")
+
+    def __enter__(self):
+        self.saved = {n: getattr(torch.Tensor, n) for n in self.NAMES}
+        for n in self.NAMES:
+            setattr(torch.Tensor, n, lambda *a, _n=n, **k: (_ for _ in ()).throw(AssertionError(f"host read {_n}")))
+
+    def __exit__(self, *exc):
+        for n, f in self.saved.items():
+            setattr(torch.Tensor, n, f)
+
+
+def test_lowering_under_capture_reads_nothing_back_and_counts_bad_rows(monkeypatch):
+    """Under HIP-graph capture (simulated on CPU) the patched core reads no tensor back, runs the padded
+    op on the lowered ranges, and gives a row whose mask it cannot express an empty range + a count."""
+    from flash_attention_cute_amd import hf_attention as hfa
+
+    calls = []
+
+    def fake_padded(q, k, v, ks, ke, qs=None, qe=None, softmax_scale=None, causal=False, window_left=-1):
+        calls.append((ks.clone(), ke.clone(), None if qs is None else qs.clone(), None if qe is None else qe.clone()))
+        return torch.zeros_like(q)
+
+    monkeypatch.setattr(hfa, "_capturing", lambda t: True)
+    monkeypatch.setattr(hfa, "flash_attn_padded_func", fake_padded)
+    hfa._MASK_ERRORS.clear()
+    total, b, h, d = 10, 3, 2, 8
+    valid = torch.zeros(b, total, dtype=torch.bool)
+    valid[:, 2:8] = True
+    mask = _static_masks(valid, 0, 8, total)[:, :, :8].clone()
+    mask[2, 0, 6, 3] = False  # row 2: a score hidden that padding does not explain
+    q, k = torch.randn(b, h, 8, d), torch.randn(b, h, total, d)
+    mod = type("M", (), {"is_causal": True})()
+    with _NoHostReads():
+        hfa._flash_attention_forward(mod, q, k, k, mask, scaling=0.3)
+    ks, ke, qs, qe = calls[-1]
+    assert ks.tolist() == [2, 2, 2] and ke.tolist() == [8, 8, 2]  # row 2: empty key range
+    assert qs.tolist() == [2, 2, 2] and qe.tolist() == [8, 8, 2]
+    assert hfa.mask_errors("cpu") == 1
+
+
+@pytest.mark.gpu
+def test_patched_llama_static_cache_decode_steps_replay_one_hip_graph(device):
+    """a left-padded greedy generation whose decode steps replay ONE captured
+    HIP graph of the patched model's decode step (StaticCache, TRUST_PADDING_MASK left False, the mask
+    lowered on the device) produces the token ids of unpatched transformers' eager generate."""
+    from transformers import StaticCache
+
+    from flash_attention_cute_amd import _debug
+
+    _debug.set_knobs()
+    assert hf_attention.TRUST_PADDING_MASK is False
+    model, ids, mask = tiny_generator(device, True)
+    model = model.half()
+    n_new = 24
+    with torch.no_grad():
+        ref = model.generate(ids, attention_mask=mask, max_new_tokens=n_new, do_sample=False, pad_token_id=0,
+                             cache_implementation="static")
+    b, n0 = ids.shape
+    total = n0 + n_new
+    cache = StaticCache(config=model.config, max_cache_len=total)
+    full = torch.zeros(b, total, dtype=torch.long, device=device)  # the 2-D mask over every slot
+    full[:, :n0] = mask
+    pid = (mask.long().cumsum(1) - 1).clamp(min=0)
+    toks = []
+    with torch.no_grad(), warnings.catch_warnings(), patched(ml.LlamaAttention):
+        warnings.simplefilter("ignore")
+        out = model(ids, attention_mask=full[:, :n0], position_ids=pid, past_key_values=cache, use_cache=True)
+        toks.append(out.logits[:, -1].argmax(-1, keepdim=True))
+        tok_buf, pos_buf = toks[-1].clone(), pid[:, -1:] + 1
+        full[:, n0] = 1
+
+        def step():
+            return model(tok_buf, attention_mask=full, position_ids=pos_buf, past_key_values=cache,
+                         use_cache=True).logits[:, -1]
+
+        def advance(logits, i):  # token i + 1 generated: feed it at the next slot
+            toks.append(logits.argmax(-1, keepdim=True))
+            tok_buf.copy_(toks[-1])
+            full[:, n0 + i] = 1
+            pos_buf.add_(1)
+
+        advance(step(), 1)  # decode step 1 eagerly (it also warms every lazy initialisation up)
+        torch.cuda.synchronize()
+        errors0 = hf_attention.mask_errors(device)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            logits_buf = step()
+        assert _debug.last_path() in ("decode", "decode_split"), _debug.last_path()
+        for i in range(2, n_new):
+            graph.replay()
+            advance(logits_buf, i)
+        torch.cuda.synchronize()
+    got = torch.cat([ids] + toks[:n_new], dim=1)
+    assert got.shape == ref.shape
+    assert torch.equal(got, ref), (got[:, n0:], ref[:, n0:])
+    assert hf_attention.mask_errors(device) == errors0 == 0

@@ -269,3 +269,60 @@ def test_padded_decode_graph_capture(padded_op, device):
     ref, path = padded_op(q, k, v, ks, ke)
     assert path in ("decode", "decode_split")
     assert torch.equal(out, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("causal", [False, True])
+def test_padded_prefill_seqlen_sliced_q(padded_op, device, causal):
+    """q a seqlen slice of a longer buffer (not dense): empty_like would give a contiguous o with a
+    different rows-per-batch multiple than q, so the binding makes q contiguous."""
+    b, hq, hkv, sq, sk, d = 3, 8, 2, 200, 200, 128
+    q, k, v = make_batch(b, hq, hkv, sq + 56, sk, d, torch.float16, 19, "bhsd")
+    q = q[:, :, :sq]
+    assert not q.is_contiguous()
+    ks, ke, qs, qe = ranges(b, sq, sk, 19, "left", min_len=30)
+    dv = lambda t: t.to(device)  # noqa: E731
+    out, path = padded_op(dv(q), dv(k), dv(v), dv(ks), dv(ke), dv(qs), dv(qe), causal=causal)
+    torch.cuda.synchronize()
+    assert path == "w4"
+    check_padded(out, oracle_padded(q, k, v, ks, ke, qs, qe, d ** -0.5, causal), torch.float16)
+
+
+@pytest.mark.gpu
+def test_padded_out_of_range_positions_are_clamped(padded_op, device):
+    """Ranges past the tensors (negative starts, ends past Sq / Sk, end < start) are clamped on the
+    device (include/fa_gfx950.h): the result equals the call with the clamped ranges, and nothing
+    outside the output tensor is written (guard rows around it stay untouched)."""
+    b, hq, hkv, s, d = 4, 8, 2, 300, 128
+    q, k, v = make_batch(b, hq, hkv, s, s, d, torch.bfloat16, 23, "bhsd")
+    bad = [torch.tensor(x, dtype=torch.int32) for x in
+           ([-50, 10, 290, 400], [250, 900, 280, 500], [-5, 0, 100, 301], [320, 300, 90, 1000])]
+    ks, ke, qs, qe = bad
+    clamp = lambda a, lo, hi: torch.minimum(torch.maximum(a, lo), hi)  # noqa: E731
+    z, n = torch.zeros(b, dtype=torch.int32), torch.full((b,), s, dtype=torch.int32)
+    ks_c, qs_c = clamp(ks, z, n), clamp(qs, z, n)
+    ke_c, qe_c = clamp(ke, ks_c, n), clamp(qe, qs_c, n)
+    dv = lambda t: t.to(device)  # noqa: E731
+    # q / k / v with guard rows on both sides inside one allocation, NaN-poisoned
+    def guarded(t):
+        buf = torch.full((t.shape[0], t.shape[1], t.shape[2] + 64, d), float("nan"), dtype=t.dtype, device=device)
+        buf[:, :, 32:32 + t.shape[2]] = dv(t)
+        return buf, buf[:, :, 32:32 + t.shape[2]]
+    _, qg = guarded(q)
+    _, kg = guarded(k)
+    _, vg = guarded(v)
+    for causal in (False, True):
+        out, path = padded_op(qg, kg, vg, dv(ks), dv(ke), dv(qs), dv(qe), causal=causal)
+        ref, _ = padded_op(qg, kg, vg, dv(ks_c), dv(ke_c), dv(qs_c), dv(qe_c), causal=causal)
+        torch.cuda.synchronize()
+        assert path == "w4"
+        assert torch.isfinite(out).all()  # the NaN guard rows were never read
+        assert torch.equal(out, ref)
+        check_padded(out, oracle_padded(q, k, v, ks_c, ke_c, qs_c, qe_c, d ** -0.5, causal), torch.bfloat16)
+    # decode (Sq == 1, split-KV kernel): key ranges clamped the same way
+    q1 = qg[:, :, -1:]
+    out1, path1 = padded_op(q1, kg, vg, dv(ks), dv(ke), causal=True)
+    ref1, _ = padded_op(q1, kg, vg, dv(ks_c), dv(ke_c), causal=True)
+    torch.cuda.synchronize()
+    assert path1 in ("decode", "decode_split")
+    assert torch.isfinite(out1).all() and torch.equal(out1, ref1)

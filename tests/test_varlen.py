@@ -102,9 +102,10 @@ def test_varlen_max_seqlen_check(monkeypatch):
         fam._check_varlen_maxima(cu_q, cu_k, mq - 1, mk)
     with pytest.raises(ValueError, match="max_seqlen_k"):
         fam._check_varlen_maxima(cu_q, cu_k, mq, mk - 1)
-    monkeypatch.setattr(fam, "_CHECK_VARLEN", True)
+    monkeypatch.setenv("FA_CHECK_VARLEN", "1")  # set after import: read at the call
     with pytest.raises(ValueError):
         fam.flash_attn_varlen_func(q, k, v, cu_q, cu_k, mq - 1, mk)
+    monkeypatch.setenv("FA_CHECK_VARLEN", "0")
 
 
 def test_varlen_op_registration():
