@@ -13,10 +13,18 @@ inputs and stores inputs + outputs as fixtures:
                      top-left CPU causal equals the kernel's bottom-right causal)
   golden_multi.npz   fp16 / bf16 cases at multi-block sizes (see MULTI_SPEC): several Q blocks and
                      >= 10 KV tiles, Sq != Sk, Sq == 1, D in {40, 72, 100}, a strided input
+  golden_gqa.npz     GQA / MQA cases (see GQA_SPEC): the reference's CPU path raises on GQA, so the
+                     reference op is called on K/V expanded with ``repeat_interleave`` over the
+                     q-heads of each group -- exactly how the reference's own harness expresses GQA
+                     (reference scripts/benchmark_kernel.py:37-38), the same head mapping as the
+                     kernel's ``head / head_q_per_group`` (reference
+                     csrc/flash_attention_template.cuh:157-160); the UNEXPANDED inputs are stored.
+                     Sq == 1 cases are the GPU's q-head pack (reference
+                     csrc/flash_attention_api.cpp:72-83) with g = 4 and g = 8.
   golden_meta.json   the op schema and the reference's error on a GQA call on CPU
 
 No bytecode is written into /root/reference. Re-run with:  python tests/golden/make_golden.py
-(``--multi`` regenerates only golden_multi.npz).
+(``--multi`` / ``--gqa`` regenerate only golden_multi.npz / golden_gqa.npz).
 """
 from __future__ import annotations
 
@@ -95,8 +103,51 @@ def make_multi(ref) -> int:
     return len(MULTI_SPEC)
 
 
+# GQA cases (golden_gqa.npz). Inputs are small integers / 4 (exact in fp16 and bf16), stored as int8
+# codes to keep the file under 1 MB; outputs as the reference returned them. Causal only with Sq == Sk
+# (the reference's CPU path is top-left causal); Sq == 1 non-causal (the reference's GPU pack forces it).
+#  (name, dtype, B, Hq, Hkv, Sq, Sk, D, causal)
+GQA_SPEC = [
+    ("f16", torch.float16, 1, 8, 2, 384, 384, 64, True),     # g = 4: 2 Q blocks (one ragged), 6 KV tiles
+    ("bf16", torch.bfloat16, 1, 4, 2, 300, 300, 64, False),  # g = 2
+    ("f16", torch.float16, 2, 8, 2, 1, 256, 64, False),      # decode pack, g = 4
+    ("bf16", torch.bfloat16, 1, 16, 2, 1, 300, 64, False),   # decode pack, g = 8
+    ("bf16", torch.bfloat16, 1, 32, 8, 1, 128, 64, False),   # decode pack at Llama-3-8B's Hq32 / Hkv8
+]
+GQA_CODE_SCALE = 4.0
+
+
+def make_gqa(ref) -> int:
+    cases = {}
+    for i, (name, dt, b, hq, hkv, sq, sk, d, causal) in enumerate(GQA_SPEC):
+        gen = torch.Generator().manual_seed(2000 + i)
+        codes = [torch.randint(-8, 8, (b, h, s, d), generator=gen, dtype=torch.int8)
+                 for h, s in ((hq, sq), (hkv, sk), (hkv, sk))]
+        q, k, v = (c.to(dt) / GQA_CODE_SCALE for c in codes)  # exact: |code| <= 8, power-of-two scale
+        g = hq // hkv
+        # the reference harness's GQA expansion (scripts/benchmark_kernel.py:37-38): q-head h reads
+        # kv-head h // g
+        o = ref.flash_attn_func(q, k.repeat_interleave(g, dim=1), v.repeat_interleave(g, dim=1), causal=causal)
+        key = f"case{i}"
+        cases[f"{key}_qc"], cases[f"{key}_kc"], cases[f"{key}_vc"] = (c.numpy() for c in codes)
+        cases[f"{key}_o"] = to_np(o.contiguous())
+        cases[f"{key}_meta"] = np.array([b, hq, hkv, sq, sk, d, int(causal)], dtype=np.int64)
+        cases[f"{key}_dtype"] = np.array(name)
+        cases[f"{key}_scale"] = np.float64(d ** -0.5)
+    cases["code_scale"] = np.float64(GQA_CODE_SCALE)
+    np.savez_compressed(OUT / "golden_gqa.npz", **cases)
+    return len(GQA_SPEC)
+
+
 def main() -> None:
     ref = import_reference_op()
+    if "--gqa" in sys.argv:  # regenerate only golden_gqa.npz (+ its count in golden_meta.json)
+        warnings.simplefilter("ignore")
+        meta = json.loads((OUT / "golden_meta.json").read_text())
+        meta["n_gqa_cases"] = make_gqa(ref)
+        (OUT / "golden_meta.json").write_text(json.dumps(meta, indent=1) + "\n")
+        print(json.dumps(meta, indent=1))
+        return
     if "--multi" in sys.argv:  # regenerate only golden_multi.npz (+ its count in golden_meta.json)
         warnings.simplefilter("ignore")
         meta = json.loads((OUT / "golden_meta.json").read_text())
@@ -143,6 +194,7 @@ def main() -> None:
     except RuntimeError as e:
         gqa_err = str(e).splitlines()[0]
     meta = {"schema": schema, "cpu_gqa_error": gqa_err, "n_small_cases": len(spec), "n_multi_cases": make_multi(ref),
+            "n_gqa_cases": make_gqa(ref),
             "generator": "reference flash_attention/flash_attention.py CPU path, torch " + torch.__version__}
     (OUT / "golden_meta.json").write_text(json.dumps(meta, indent=1) + "\n")
     print(json.dumps(meta, indent=1))

@@ -97,6 +97,35 @@ def test_reference_golden_multi_block_vectors_on_gpu(op, device):
     assert all(p == "w4" for p, s in zip(paths, metas) if s > 1), paths
 
 
+def test_reference_golden_gqa_vectors_on_gpu(op, device):
+    """GQA and the Sq == 1 q-head pack pinned to the REFERENCE's outputs (tests/golden/golden_gqa.npz:
+    the reference op on K / V expanded with repeat_interleave, reference scripts/benchmark_kernel.py:
+    37-38): unexpanded K / V through the HIP op -- prefill on the persistent kernel with kv-head h // g
+    (reference csrc/flash_attention_template.cuh:157-160), Sq == 1 with g = 4 and g = 8 on the decode
+    kernel behind the reference's pack (reference csrc/flash_attention_api.cpp:72-83)."""
+    from flash_attention_cute_amd import _debug
+
+    g = np.load(GOLD / "golden_gqa.npz")
+    n = json.loads((GOLD / "golden_meta.json").read_text())["n_gqa_cases"]
+    assert n == 5
+    cs = float(g["code_scale"])
+    paths = {}
+    for i in range(n):
+        dtype = str(g[f"case{i}_dtype"])
+        b, hq, hkv, sq, sk, d, causal = (int(x) for x in g[f"case{i}_meta"])
+        tdt = torch.float16 if dtype == "f16" else torch.bfloat16
+        q, k, v = (torch.from_numpy(g[f"case{i}_{n_}c"]).to(tdt).div_(cs).to(device) for n_ in "qkv")
+        ref = _gold_tensor(g[f"case{i}_o"], dtype).float()
+        out = op(q, k, v, causal=bool(causal)).float().cpu()
+        paths[(sq, hq // hkv)] = _debug.last_path()
+        tol = {"f16": 2e-3, "bf16": 1.6e-2}[dtype]
+        err = (out - ref).abs()
+        assert (err <= tol + tol * ref.abs()).all(), (i, err.max().item())
+        assert err.mean().item() < tol / 8, (i, err.mean().item())
+    assert paths[(1, 4)].startswith("decode") and paths[(1, 8)].startswith("decode"), paths
+    assert all(p == "w4" for (sq, _), p in paths.items() if sq > 1), paths
+
+
 @pytest.mark.parametrize("causal", [False, True])
 def test_reference_module_path_pybind_call_matches_flash_attn_func(op, device, causal):
     """Code written against the reference's submodule: ``flash_attention.flash_attention

@@ -160,3 +160,43 @@ def test_flops_and_bytes_formulas():
     assert O.attention_flops(4, 32, 8192, 8192, 128, True) == pytest.approx(2.1990e12, rel=1e-4)
     assert O.attention_bytes(4, 32, 32, 4096, 4096, 128, 2) == 536870912
     assert O.attention_bytes(4, 32, 8, 4096, 4096, 128, 2) == 335544320
+
+
+def load_gqa_case(g, i):
+    """(q, k, v, o) float64 (q / o [B, Hq, Sq, D], k / v [B, Hkv, Sk, D] -- NOT expanded), dtype, scale,
+    causal, (Hq, Hkv) of golden_gqa case i (tests/golden/make_golden.py: the reference op on K / V
+    expanded with repeat_interleave, reference scripts/benchmark_kernel.py:37-38)."""
+    dtype = str(g[f"case{i}_dtype"])
+    b, hq, hkv, sq, sk, d, causal = (int(x) for x in g[f"case{i}_meta"])
+    cs = float(g["code_scale"])
+    q, k, v = (g[f"case{i}_{n}c"].astype(np.float64) / cs for n in "qkv")
+    o = as_f64(g[f"case{i}_o"], dtype)
+    assert q.shape == (b, hq, sq, d) and k.shape == (b, hkv, sk, d) and o.shape == q.shape
+    return q, k, v, o, dtype, float(g[f"case{i}_scale"]), bool(causal), (hq, hkv)
+
+
+@pytest.mark.parametrize("i", range(json.loads((GOLD / "golden_meta.json").read_text())["n_gqa_cases"]))
+def test_golden_gqa_cases(i):
+    """GQA / MQA and the Sq == 1 q-head pack with g = 4 and g = 8 against the reference op's outputs:
+    the restatement's kv-head mapping h // g (reference csrc/flash_attention_template.cuh:157-160) and
+    pack (reference csrc/flash_attention_api.cpp:72-83) reproduce the reference on unexpanded K / V."""
+    g = np.load(GOLD / "golden_gqa.npz")
+    q, k, v, o, dtype, scale, causal, _ = load_gqa_case(g, i)
+    out = O.flash_attention_fwd(q, k, v, scale, causal, dtype)
+    atol = {"f16": 2e-3, "bf16": 1.6e-2}[dtype]
+    np.testing.assert_allclose(out, o, atol=atol, rtol=atol)
+    assert np.abs(out - o).mean() < atol / 8
+
+
+def test_golden_gqa_covers_the_pack_and_the_mapping():
+    g = np.load(GOLD / "golden_gqa.npz")
+    n = json.loads((GOLD / "golden_meta.json").read_text())["n_gqa_cases"]
+    metas = [tuple(int(x) for x in g[f"case{i}_meta"]) for i in range(n)]
+    assert {hq // hkv for _, hq, hkv, sq, *_ in metas if sq == 1} >= {4, 8}  # the pack at g = 4 and 8
+    assert any(sq > 256 and hkv > 1 and c for _, hq, hkv, sq, sk, _, c in metas)  # causal GQA, >= 2 Q blocks
+    assert any(hq == 32 and hkv == 8 for _, hq, hkv, *_ in metas)
+    assert (GOLD / "golden_gqa.npz").stat().st_size <= 1 << 20
+    # the mapping matters: the same case with q-head h reading kv-head h % Hkv gives other outputs
+    q, k, v, o, dtype, scale, causal, (hq, hkv) = load_gqa_case(g, 0)
+    wrong = O.flash_attention_fwd(q, k[:, np.arange(hq) % hkv], v[:, np.arange(hq) % hkv], scale, causal, dtype)
+    assert np.abs(wrong - o).max() > 0.1
