@@ -32,6 +32,9 @@ HIPCC = ROCM / "bin" / "hipcc"
 ARCH = "gfx950"
 
 ABI_LIB = LIBDIR / "libfa_gfx950.so"
+# the same C-ABI with the debug / A-B kernel bodies compiled in (-DFA_DEBUG_VARIANTS: fa_fwd_w8,
+# fa_fwd_p8, the non-pipelined w4slow body), for the GPU test sweep and A/B scripts only
+DEBUG_LIB = LIBDIR / "libfa_gfx950_debug.so"
 EXT_NAME = "_C"
 
 
@@ -75,8 +78,9 @@ def _jobs() -> int:
 
 
 def build_abi(force: bool = False, verbose: bool = False, stamps: bool = False, tag: str = "",
-              defines: tuple = (), flags: tuple = (), only: tuple = ()) -> Path:
-    """Compile the HIP kernels + C-ABI into lib/libfa_gfx950.so (gfx950 code objects).
+              defines: tuple = (), flags: tuple = (), only: tuple = (), debug: bool = False) -> Path:
+    """Compile the HIP kernels + C-ABI into lib/libfa_gfx950.so (gfx950 code objects); ``debug``:
+    lib/libfa_gfx950_debug.so, the same with the debug / A-B kernel bodies (-DFA_DEBUG_VARIANTS).
 
     Each kernel instantiation is its own translation unit (csrc/fa_inst.hip with -D selectors), so
     the 16 device compiles run in parallel; objects go to build/ and are linked by hipcc.
@@ -87,14 +91,17 @@ def build_abi(force: bool = False, verbose: bool = False, stamps: bool = False, 
     # (experiment builds without stamps: tag + defines, to build/exp_<tag>/, for scripts/ab_libs.py)
     sdir = ("stamps" if stamps else "exp") + (f"_{tag}" if tag else "")
     diag = stamps or bool(tag)
-    out_lib = ROOT / "build" / sdir / "libfa_gfx950.so" if diag else ABI_LIB
+    out_lib = ROOT / "build" / sdir / "libfa_gfx950.so" if diag else DEBUG_LIB if debug else ABI_LIB
     out_lib.parent.mkdir(parents=True, exist_ok=True)
     if not force and not _stale(out_lib, abi_sources()):
         return out_lib
     if not HIPCC.exists():
         raise RuntimeError(f"hipcc not found at {HIPCC}")
-    objdir = ROOT / "build" / (f"obj_{sdir}" if diag else "obj")
+    objdir = ROOT / "build" / (f"obj_{sdir}" if diag else "obj_debug" if debug else "obj")
     extra = ((["-DFA_STAMPS=1"] if stamps else []) + [f"-D{d}" for d in defines] + list(flags)) if diag else []
+    if debug or stamps:  # (stamp builds keep the debug bodies: scripts/stamps.py can select p8; experiment
+        # builds compile what the product does, so an A/B against the product library compares like code)
+        extra = ["-DFA_DEBUG_VARIANTS=1"] + extra
     objdir.mkdir(parents=True, exist_ok=True)
     cmds = []
     objs = []
@@ -167,6 +174,7 @@ def build_ext(force: bool = False, verbose: bool = False) -> Path:
 
 def build_all(force: bool = False, verbose: bool = False) -> None:
     build_abi(force=force, verbose=verbose)
+    build_abi(force=force, verbose=verbose, debug=True)
     build_ext(force=force, verbose=verbose)
 
 

@@ -1,9 +1,16 @@
 """Diagnostic hooks of the C-ABI library (not part of include/fa_gfx950.h; tests and A/B scripts).
 
 The dispatcher reads its tuning / debug knobs ONCE per process (from the environment, at the first
-launch) and never per launch (csrc/fa_launch.h ``Knobs``). Tests that need another kernel variant or
-grid cap switch them with :func:`knobs`, which restores the defaults on exit, and check which kernel
-actually ran with :func:`last_path`.
+launch) and never per launch (csrc/fa_launch.h ``Knobs``). Tests that need another grid cap or the
+decode kernel off switch them with :func:`knobs`, which restores the defaults on exit, and check
+which kernel actually ran with :func:`last_path`.
+
+The debug / A-B kernel bodies (``fa_fwd_w8``, ``fa_fwd_p8``, the non-pipelined ``w4slow`` body) are
+NOT in the product library the op loads: they live in ``lib/libfa_gfx950_debug.so`` (the same
+C-ABI built with -DFA_DEBUG_VARIANTS). :func:`forward` runs one of them through that library's
+C-ABI with the host steps of the op restated (default scale, head-dim pad, the Sq == 1 q-head pack
+of reference csrc/flash_attention_api.cpp:72-83, the stride-preserving output), for the GPU parity
+sweep.
 """
 from __future__ import annotations
 
@@ -14,42 +21,101 @@ from . import _build
 
 PATHS = {0: "none", 1: "w4", 2: "w8", 3: "w4slow", 4: "decode", 5: "decode_split", 6: "p8"}
 VARIANTS = {"w4": 0, "w8": 1, "w4slow": 2, "p8": 3}
+LOG2E = 1.4426950408889634
 
-_lib = None
+_libs = {}
 
 
-def lib() -> ctypes.CDLL:
-    """The already-loaded libfa_gfx950.so (the torch binding links it; dlopen returns that handle)."""
-    global _lib
-    if _lib is None:
+class FaFwdParams(ctypes.Structure):
+    """include/fa_gfx950.h ``fa_fwd_params`` (field order of reference csrc/flash_attention.h:5-37)."""
+
+    _fields_ = ([(n, ctypes.c_void_p) for n in ("q_ptr", "k_ptr", "v_ptr", "o_ptr")]
+                + [(n, ctypes.c_int64) for n in ("batch_size", "num_heads_q", "num_heads_kv", "seqlen_q", "seqlen_kv",
+                                                 "headdim", "head_q_per_group")]
+                + [(f"{t}_{s}_stride", ctypes.c_int64) for s in ("batch", "head", "seqlen") for t in "qkvo"]
+                + [("softmax_scale", ctypes.c_float)])
+
+
+def lib(debug: bool = False) -> ctypes.CDLL:
+    """The already-loaded libfa_gfx950.so (the torch binding links it; dlopen returns that handle), or
+    (``debug``) lib/libfa_gfx950_debug.so."""
+    if debug not in _libs:
         import torch  # noqa: F401  -- the HIP runtime first, as in the product
 
-        lib = ctypes.CDLL(str(_build.ABI_LIB))
+        path = _build.DEBUG_LIB if debug else _build.ABI_LIB
+        if not path.exists():
+            raise RuntimeError(f"{path} is missing: run __graft_entry__.build()")
+        lib = ctypes.CDLL(str(path))
         lib.fa_debug_set_knobs.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int64, ctypes.c_int]
         lib.fa_debug_set_knobs.restype = None
         lib.fa_debug_last_path.restype = ctypes.c_int
-        _lib = lib
-    return _lib
+        lib.fa_last_error.restype = ctypes.c_char_p
+        _libs[debug] = lib
+    return _libs[debug]
 
 
 def set_knobs(variant: str | None = None, w4_grid: int | None = None, decode: bool | None = None,
-              dec_target: int | None = None, dec_flags: int | None = None) -> None:
-    """Override knobs for the following launches; None restores that knob's default."""
-    lib().fa_debug_set_knobs(-1 if variant is None else VARIANTS[variant], -1 if w4_grid is None else int(w4_grid),
-                             -1 if decode is None else int(bool(decode)), -1 if dec_target is None else int(dec_target),
-                             -1 if dec_flags is None else int(dec_flags))
+              dec_target: int | None = None, dec_flags: int | None = None, debug: bool = False) -> None:
+    """Override knobs for the following launches; None restores that knob's default. ``variant`` other
+    than w4 exists only in the debug library."""
+    if variant not in (None, "w4") and not debug:
+        raise ValueError(f"variant {variant!r} is only in the debug library (debug=True, forward())")
+    lib(debug).fa_debug_set_knobs(-1 if variant is None else VARIANTS[variant],
+                                  -1 if w4_grid is None else int(w4_grid),
+                                  -1 if decode is None else int(bool(decode)),
+                                  -1 if dec_target is None else int(dec_target),
+                                  -1 if dec_flags is None else int(dec_flags))
 
 
 @contextlib.contextmanager
-def knobs(**kw):
-    """``with knobs(variant="w8"): ...`` -- every knob back to its default afterwards."""
-    set_knobs(**kw)
+def knobs(debug: bool = False, **kw):
+    """``with knobs(w4_grid=16): ...`` -- every knob back to its default afterwards."""
+    set_knobs(debug=debug, **kw)
     try:
         yield
     finally:
-        set_knobs()
+        set_knobs(debug=debug)
 
 
-def last_path() -> str:
-    """Kernel the last op call on this thread launched ("w4", "decode_split", ...)."""
-    return PATHS.get(lib().fa_debug_last_path(), "unknown")
+def last_path(debug: bool = False) -> str:
+    """Kernel the last call on this thread launched ("w4", "decode_split", ...)."""
+    return PATHS.get(lib(debug).fa_debug_last_path(), "unknown")
+
+
+def forward(q, k, v, softmax_scale=None, causal=False, variant="w8", window_left=-1, w4_grid=None):
+    """Attention through a kernel body of the DEBUG library (tests: the parity sweep over w8 / w4slow /
+    p8): the op's host steps (reference flash_attention/flash_attention.py:17-53 and
+    csrc/flash_attention_api.cpp:64-133, restated) over lib/libfa_gfx950_debug.so's C-ABI."""
+    import torch
+
+    dl = lib(debug=True)
+    set_knobs(variant=variant, w4_grid=w4_grid, debug=True)
+    d0 = q.size(-1)
+    scale = d0 ** -0.5 if softmax_scale is None else softmax_scale
+    if d0 % 8:
+        pad = [0, 8 - d0 % 8]
+        q, k, v = (torch.nn.functional.pad(t, pad) for t in (q, k, v))
+    q, k, v = (t if t.stride(3) == 1 else t.contiguous() for t in (q, k, v))
+    b, hq, sq, d = q.shape
+    hkv, sk = k.size(1), k.size(2)
+    g = hq // hkv
+    qx = q
+    pack = sq == 1 and window_left < 0
+    if pack:  # the q-heads of a kv group become the rows of one (batch, kv-head) problem
+        qx = q.reshape(b, hkv, g, d)
+        causal = False
+    o = torch.empty_like(qx)
+    st = lambda t, i: t.stride(i) if t.size(i) > 1 else 0  # noqa: E731
+    p = FaFwdParams(qx.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), b, qx.size(1), hkv, qx.size(2), sk, d,
+                    1 if pack else g, *(st(t, i) for i in range(3) for t in (qx, k, v, o)),
+                    float(torch.tensor(scale, dtype=torch.float32).double() * LOG2E))
+    dtype = 0 if q.dtype == torch.float16 else 1
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    if window_left >= 0:
+        rc = dl.fa_fwd_gfx950_window(ctypes.byref(p), dtype, int(causal), ctypes.c_int64(window_left), stream)
+    else:
+        rc = dl.fa_fwd_gfx950(ctypes.byref(p), dtype, int(causal), stream)
+    if rc != 0:
+        raise RuntimeError(f"debug library call failed ({rc}): {dl.fa_last_error().decode()}")
+    o = o.reshape(q.shape)
+    return o[..., :d0] if d0 % 8 else o

@@ -42,11 +42,21 @@ fa::Knobs knobs_from_env() {
     if (const char *e = getenv("FA_GFX950_DECODE")) k.decode = strcmp(e, "0") != 0;
     if (const char *e = getenv("FA_DEC_TARGET_WGS")) k.dec_target = atoll(e) > 0 ? atoll(e) : fa::kDecTargetWgs;
     if (const char *e = getenv("FA_DEC_FLAGS")) k.dec_flags = atoi(e);
+#ifdef FA_DEBUG_VARIANTS
     if (k.variant != 0)  // a debug / A-B body replaces the product kernel for the whole process: say so
         fprintf(stderr,
                 "[fa_gfx950] FA_GFX950_VARIANT=%s: prefill launches run the %s kernel instead of fa_fwd_w4 "
                 "(debug / A-B variant, not the product path)\n",
                 getenv("FA_GFX950_VARIANT"), k.variant == 1 ? "fa_fwd_w8" : k.variant == 2 ? "w4slow" : "fa_fwd_p8");
+#else
+    if (k.variant != 0) {  // the product library compiles fa_fwd_w4 only
+        fprintf(stderr,
+                "[fa_gfx950] FA_GFX950_VARIANT=%s ignored: the debug / A-B kernel bodies are only in "
+                "lib/libfa_gfx950_debug.so (built with -DFA_DEBUG_VARIANTS)\n",
+                getenv("FA_GFX950_VARIANT"));
+        k.variant = 0;
+    }
+#endif
     return k;
 }
 const fa::Knobs &env_defaults() {
@@ -70,7 +80,11 @@ void fa::set_last_path(int path) { g_last_path = path; }
 extern "C" void fa_debug_set_knobs(int variant, int64_t w4_grid, int decode, int64_t dec_target, int dec_flags) {
     const fa::Knobs &d = env_defaults();
     fa::Knobs &k = knobs_mut();
+#ifdef FA_DEBUG_VARIANTS
     k.variant = variant < 0 ? d.variant : variant;
+#else
+    (void)variant;  // (fa_fwd_w4 only in the product library)
+#endif
     k.w4_grid = w4_grid < 0 ? d.w4_grid : w4_grid;
     k.decode = decode < 0 ? d.decode : decode;
     k.dec_target = dec_target <= 0 ? d.dec_target : dec_target;

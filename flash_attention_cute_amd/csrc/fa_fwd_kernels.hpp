@@ -261,6 +261,7 @@ __device__ __forceinline__ Work decode_work(const uint32_t nwg, const uint32_t b
     return r;
 }
 
+#ifdef FA_DEBUG_VARIANTS  // (debug / A-B library only: _build.build_abi(debug=True))
 template <class DT, bool kCausal, int kD, bool kExactD>
 __global__ __launch_bounds__(kThreads) void fa_fwd_w8(const fa_fwd_params p, const int n_qtiles) {
     using G = Geo<kD>;
@@ -533,6 +534,8 @@ __global__ __launch_bounds__(kThreads) void fa_fwd_w8(const fa_fwd_params p, con
     }
 }
 
+
+#endif  // FA_DEBUG_VARIANTS
 
 // =============================================================================================
 // fa_fwd_w4: one wave per SIMD, 64 query rows per wave (two 32-row blocks A and B), software
@@ -1617,7 +1620,12 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // Tile j runs with parity (j - j_lo) & 1 (ring slots and S / P registers). A local window adds
     // a leading run of masked tiles [j_lo, j_um), rounded up to an even count so the unmasked loop
     // starts on parity 0.
+#ifdef FA_DEBUG_VARIANTS
     const int n_loop = (dbg & 1) ? j_lo : n_end;
+#else
+    (void)dbg;  // (the product library has no debug body: every tile runs pipelined)
+    const int n_loop = n_end;
+#endif
     const int n_unm = min(n_pipe, n_loop);
     int j = j_lo;  // the next tile
     if (j_um > j_lo) {
@@ -1660,6 +1668,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     }
     const bool last_dead = kCausal && n_loop > max(jA, j_lo);  // the last pipelined tile is A-dead
     FA_STAMP(s_loop_end);
+#ifdef FA_DEBUG_VARIANTS
     // ---- debug variant: every tile masked, not pipelined -----------------------------------
     if (n_loop < n_end) {
         stage_v(n_loop, (n_loop - j_lo) & 1);  // the pipeline fetched V one tile late; catch up first
@@ -1687,6 +1696,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         dma_wait();
         __syncthreads();
     }
+
+#endif  // FA_DEBUG_VARIANTS
 
     // ---- next block: its Q fragments and K_0 go in flight under this block's drain and stores.
     // Every wave is past this block's last barrier: the Q AGPRs and both K slots are free (the
@@ -1793,9 +1804,11 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 }
 #undef FA_STAMP
 
+#ifdef FA_DEBUG_VARIANTS
 // the paired 8-wave kernel (fa_fwd_p8.hpp)
 template <class DT, bool C, int kD, bool kExact>
 int launch_p8(const fa_fwd_params &p, hipStream_t stream);
+#endif
 
 // ---- host launch of one instantiation -------------------------------------------------
 template <class DT, bool C, int kD, bool kExact>
@@ -1805,6 +1818,7 @@ int launch_one(const fa_fwd_params &p, const PathArgs &xa, hipStream_t stream) {
     const int64_t nwg = n_qtiles * p.num_heads_q * p.batch_size;
     // varlen, fused RoPE and the local window run fa_fwd_w4 (w4slow under the debug variant); w8 / p8
     // have none of them
+#ifdef FA_DEBUG_VARIANTS
     const bool w4_only = xa.k_rng || xa.cos || xa.window_left >= 0;
     const int variant = w4_only && (variant_from_env() == 1 || variant_from_env() == 3) ? 0 : variant_from_env();
     if (variant == 3) return launch_p8<DT, C, kD, kExact>(p, stream);
@@ -1812,6 +1826,9 @@ int launch_one(const fa_fwd_params &p, const PathArgs &xa, hipStream_t stream) {
         hipLaunchKernelGGL((fa_fwd_w8<DT, C, kD, kExact>), dim3((uint32_t)nwg), dim3(kThreads), 0, stream, p,
                            (int)n_qtiles);
     else
+#else
+    constexpr int variant = 0;  // the product library: fa_fwd_w4 only
+#endif
         // persistent: about one workgroup per CU (the kernel walks the Q blocks itself)
         hipLaunchKernelGGL((fa_fwd_w4<DT, C, kD, kExact>), dim3((uint32_t)w4_grid(nwg)), dim3(256), 0, stream, p,
                            (int)n_qtiles, variant == 2 ? 1 : 0, stamp_buffer(), xa);

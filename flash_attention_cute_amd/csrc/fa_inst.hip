@@ -3,7 +3,9 @@
 // FA_INST_EXACT (0 | 1), in parallel, and links the objects with fa_fwd_gfx950.hip.
 #ifndef FA_INST_STUB
 #include "fa_fwd_kernels.hpp"
+#ifdef FA_DEBUG_VARIANTS  // (the debug / A-B library: the paired 8-wave body)
 #include "fa_fwd_p8.hpp"
+#endif
 #include "fa_decode.hpp"
 #else
 // diagnostic builds that only need some instantiations (_build.build_abi(only=...)): the others

@@ -209,13 +209,19 @@ def test_knobs_are_set_through_the_debug_hook_not_per_launch_env(lib, monkeypatc
     from flash_attention_cute_amd import _debug
 
     _debug.set_knobs()
+    dlib = _debug.lib(debug=True)  # the debug / A-B library (-DFA_DEBUG_VARIANTS), its knobs read now
+    dlib.fa_fwd_gfx950_geometry.restype = ctypes.c_int
+    assert geometry(dlib, good_params())[2] == 256
     monkeypatch.setenv("FA_GFX950_VARIANT", "w8")
     monkeypatch.setenv("FA_GFX950_DECODE", "0")
     assert geometry(lib, good_params())[2] == 256          # still fa_fwd_w4 (4 waves)
     assert geometry(lib, decode_params())[0] == 32         # still the decode kernel
-    with _debug.knobs(variant="w8"):
-        assert geometry(lib, good_params())[2] == 512      # fa_fwd_w8: 8 waves
-        assert geometry(lib, decode_params())[0] == 256    # variants other than w4 never use decode
+    with pytest.raises(ValueError):  # the product library compiles fa_fwd_w4 only
+        _debug.set_knobs(variant="w8")
+    with _debug.knobs(variant="w8", debug=True):
+        assert geometry(dlib, good_params())[2] == 512      # fa_fwd_w8: 8 waves
+        assert geometry(dlib, decode_params())[0] == 256    # variants other than w4 never use decode
+    assert geometry(dlib, good_params())[2] == 256
     with _debug.knobs(decode=False):
         assert geometry(lib, decode_params())[0] == 256
     assert geometry(lib, good_params())[2] == 256 and geometry(lib, decode_params())[0] == 32
@@ -331,3 +337,46 @@ def test_padded_entry_validates_before_touching_the_device(lib):
     assert lib.fa_fwd_gfx950_padded(ctypes.byref(bad), 0, 1, -1, None, 0, None) == FA_ERR_UNSUPPORTED
     assert lib.fa_fwd_gfx950_padded_workspace_size(ctypes.byref(bad), 0, 1, -1) == -1
     assert lib.fa_fwd_gfx950_padded(None, 0, 1, -1, None, 0, None) == FA_ERR_INVALID_ARGUMENT
+
+
+def test_debug_bodies_only_in_the_debug_library():
+    """The product library compiles fa_fwd_w4 (+ decode) only; fa_fwd_w8 / fa_fwd_p8 and the
+    non-pipelined w4slow body are in lib/libfa_gfx950_debug.so (-DFA_DEBUG_VARIANTS)."""
+    from flash_attention_cute_amd import _build
+
+    prod = LIB.read_bytes()
+    assert b"fa_fwd_w4" in prod and b"fa_fwd_w8" not in prod and b"fa_fwd_p8" not in prod
+    dbg = _build.DEBUG_LIB.read_bytes()
+    assert b"fa_fwd_w4" in dbg and b"fa_fwd_w8" in dbg and b"fa_fwd_p8" in dbg
+
+
+def test_host_validation_under_asan_ubsan(tmp_path):
+    """The C-ABI's host-side validation and dispatch (csrc/fa_fwd_gfx950.hip) built with
+    AddressSanitizer + UBSan on the host code only (-Xarch_host -fsanitize=...; device code is never
+    sanitized) and linked with host-only stub instantiations (tests/asan/stub_instances.hip): every
+    entry point with valid and invalid parameters returns the right code with no sanitizer report
+    (tests/asan/abi_validation_driver.cpp)."""
+    import os
+    import shutil
+
+    hipcc = "/opt/rocm/bin/hipcc"
+    if not shutil.which(hipcc):
+        pytest.skip("hipcc not available")
+    root = Path(__file__).resolve().parent.parent
+    inc = [f"-I{root / 'include'}", f"-I{root / 'flash_attention_cute_amd' / 'csrc'}"]
+    san = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+           "-Xarch_host", "-fno-sanitize-recover=undefined"]
+    base = [hipcc, "--offload-arch=gfx950", "-O1", "-g", "-std=c++17", "-fPIC", *san, *inc, "-c"]
+    objs = []
+    for src in (root / "flash_attention_cute_amd" / "csrc" / "fa_fwd_gfx950.hip",
+                root / "tests" / "asan" / "stub_instances.hip", root / "tests" / "asan" / "abi_validation_driver.cpp"):
+        obj = tmp_path / (src.stem + ".o")
+        subprocess.run([*base, str(src), "-o", str(obj)], check=True, capture_output=True)
+        objs.append(str(obj))
+    exe = tmp_path / "abi_asan"
+    subprocess.run([hipcc, "--offload-arch=gfx950", "-fsanitize=address", "-fsanitize=undefined", "-fno-gpu-sanitize",
+                    *objs, "-o", str(exe)], check=True, capture_output=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1")
+    res = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=120)
+    assert res.returncode == 0 and "abi validation ok" in res.stdout, res.stdout + res.stderr
+    assert "runtime error" not in res.stderr and "AddressSanitizer" not in res.stderr, res.stderr

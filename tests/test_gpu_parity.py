@@ -29,23 +29,39 @@ pytestmark = pytest.mark.gpu
 TOL = {torch.float16: (2e-3, 2e-3, 1e-4), torch.bfloat16: (1.6e-2, 1.6e-2, 1e-3)}
 
 
+class _Variant:
+    """A debug / A-B kernel body (w8, w4slow, p8) of lib/libfa_gfx950_debug.so through its C-ABI with
+    the op's host steps restated (flash_attention_cute_amd._debug.forward); the product library the op
+    loads compiles fa_fwd_w4 only."""
+
+    def __init__(self, variant):
+        self.variant = variant
+
+    def __call__(self, q, k, v, softmax_scale=None, causal=False):
+        from flash_attention_cute_amd import _debug
+
+        return _debug.forward(q, k, v, softmax_scale, causal, variant=self.variant)
+
+
 @pytest.fixture(params=["w4", "w8", "w4slow", "p8"])
 def fa(device, request):
-    """The public op with one kernel variant selected (the product default w4, the 8-wave cross-check
-    w8, the non-pipelined debug body w4slow, the paired 8-wave p8) through the debug knob hook.
-    Function-scoped: the knobs are restored to their defaults after every test, so no later test
-    inherits a variant."""
+    """The public op (the product kernel w4), or one of the debug library's bodies (the 8-wave
+    cross-check w8, the non-pipelined w4slow, the paired 8-wave p8). Function-scoped: the knobs are
+    restored to their defaults after every test."""
     import flash_attention_cute_amd as m
     from flash_attention_cute_amd import _debug
     from flash_attention_cute_amd import flash_attention as fam
 
     assert fam.flash_attention_cuda is not None, f"gfx950 extension failed to load: {fam._load_error!r}"
-    _debug.set_knobs(variant=request.param)
-    m.flash_attn_func.variant = request.param
-    try:
+    _debug.set_knobs()
+    if request.param == "w4":
+        m.flash_attn_func.variant = "w4"
         yield m.flash_attn_func
+        return
+    try:
+        yield _Variant(request.param)
     finally:
-        _debug.set_knobs()
+        _debug.set_knobs(debug=True)
 
 
 def assert_path(variant, hq, hkv, sq):
@@ -57,7 +73,8 @@ def assert_path(variant, hq, hkv, sq):
     if variant == "w4" and rows <= 64:
         assert _debug.last_path() in ("decode", "decode_split"), _debug.last_path()
     else:
-        assert _debug.last_path() == variant, (_debug.last_path(), variant)
+        path = _debug.last_path(debug=variant != "w4")
+        assert path == variant, (path, variant)
 
 
 def make(b, hq, hkv, sq, sk, d, dtype, seed):

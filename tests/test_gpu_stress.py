@@ -20,34 +20,50 @@ pytestmark = pytest.mark.gpu
 SEEDS = range(12)
 
 
+class _Op:
+    def __init__(self, variant):
+        self.variant = variant
+
+    def __call__(self, q, k, v, causal=False):
+        from flash_attention_cute_amd import _debug
+        from flash_attention_cute_amd import flash_attn_func
+
+        if self.variant == "w4":  # the product op
+            return flash_attn_func(q, k, v, causal=causal)
+        return _debug.forward(q, k, v, causal=causal, variant=self.variant, w4_grid=16)
+
+    def last_path(self):
+        from flash_attention_cute_amd import _debug
+
+        return _debug.last_path(debug=self.variant != "w4")
+
+
 @pytest.fixture(params=["w4", "p8"])
 def op(device, request):
     from flash_attention_cute_amd import _debug
     from flash_attention_cute_amd import flash_attention as fam
-    from flash_attention_cute_amd import flash_attn_func
 
     assert fam.flash_attention_cuda is not None, f"gfx950 extension failed to load: {fam._load_error!r}"
-    # 16 workgroups: each walks 4 Q blocks (3 block switches); the product kernel and the paired
-    # 8-wave variant
-    _debug.set_knobs(variant=request.param, w4_grid=16)
-    flash_attn_func.variant = request.param
+    # 16 workgroups: each walks 4 Q blocks (3 block switches); the product kernel, and the paired
+    # 8-wave variant of the debug library
+    _debug.set_knobs(w4_grid=16)
     try:
-        yield flash_attn_func
+        yield _Op(request.param)
     finally:
         _debug.set_knobs()
+        if request.param != "w4":
+            _debug.set_knobs(debug=True)
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16], ids=["f16", "bf16"])
 @pytest.mark.parametrize("causal", [False, True], ids=["full", "causal"])
 def test_seed_sweep_every_row(op, device, dtype, causal):
-    from flash_attention_cute_amd import _debug
-
     for seed in SEEDS:
         q, k, v = make(2, 8, 2, 1024, 1024, 128, dtype, 1000 + seed)
         qd, kd, vd = q.to(device), k.to(device), v.to(device)
         out = op(qd, kd, vd, causal=causal)
         again = op(qd, kd, vd, causal=causal)
         torch.cuda.synchronize()
-        assert _debug.last_path() == op.variant
+        assert op.last_path() == op.variant
         assert torch.equal(out, again), f"seed {seed}: two launches differ"
         check(out, q, k, v, 128 ** -0.5, causal, dtype)

@@ -86,19 +86,18 @@ def test_window_matches_oracle(wfn, device, case, causal, dtype):
 
 @pytest.mark.parametrize("variant", ["w8", "p8", "w4slow"])
 def test_window_under_other_variants(device, variant):
-    """The window runs on fa_fwd_w4 whatever prefill variant is selected (w8 / p8 have no window
-    mask), and through the debug body under w4slow."""
+    """In the debug library (lib/libfa_gfx950_debug.so) the window runs on fa_fwd_w4 whatever prefill
+    variant is selected (w8 / p8 have no window mask), and through the debug body under w4slow."""
     from flash_attention_cute_amd import _debug
-    from flash_attention_cute_amd import flash_attn_window_func
 
     q, k, v = make(1, 4, 2, 900, 900, 128, torch.float16, 11)
-    _debug.set_knobs(variant=variant)
     try:
-        out = flash_attn_window_func(q.to(device), k.to(device), v.to(device), 200, causal=True)
+        out = _debug.forward(q.to(device), k.to(device), v.to(device), causal=True, variant=variant,
+                             window_left=200)
         torch.cuda.synchronize()
-        assert _debug.last_path() == ("w4slow" if variant == "w4slow" else "w4")
+        assert _debug.last_path(debug=True) == ("w4slow" if variant == "w4slow" else "w4")
     finally:
-        _debug.set_knobs()
+        _debug.set_knobs(debug=True)
     _check(out, q, k, v, 128 ** -0.5, True, 200, torch.float16)
 
 
