@@ -212,6 +212,10 @@ def test_inputs_not_mutated(fa, device):
 
 
 def test_errors_are_runtime_errors(fa, device):
+    """The op's validation (reference csrc/flash_attention_api.cpp:17-59 messages): host code, the same
+    whatever kernel body the library carries -- checked on the product op."""
+    if fa.variant != "w4":
+        pytest.skip("host-side validation of the op: product library only")
     q = torch.randn(1, 3, 64, 64, device=device, dtype=torch.float16)
     k = torch.randn(1, 2, 64, 64, device=device, dtype=torch.float16)
     with pytest.raises(RuntimeError, match="multiple of number of heads"):
