@@ -6,7 +6,8 @@ inline asm reads and writes (csrc/fa_agpr_asm.inc); ``fa_fwd_p8`` likewise O (a0
 live across the separate asm statements, so a compiler-generated AGPR use in that range (for example
 a VGPR spill to an AGPR after a toolchain or code change) would silently corrupt the output. This
 module scans the ``-save-temps`` assembly: any use of those AGPRs (a0..a63 at D = 64) outside ``;;#ASMSTART``/``;;#ASMEND``
-inside ``fa_fwd_w4``, or any kernel with ``.vgpr_spill_count`` > 0, fails the build.
+inside ``fa_fwd_w4``, or any kernel with ``.vgpr_spill_count`` > 0, fails the build; so does a
+violation of the MFMA data-hazard rules R1-R5 around the inline-asm MFMAs (``hazards``, below).
 
 CLI: ``python -m flash_attention_cute_amd._asm_check file.s [...]``
 """
@@ -68,11 +69,243 @@ def spills(text: str) -> list[str]:
     return out
 
 
+# ---------------------------------------------------------------------------------------------------
+# MFMA data hazards of the hand-placed (inline-asm) MFMAs: hipcc's hazard recognizer inserts the wait
+# states between a visible MFMA and its neighbours, but it does not know that an inline-asm statement
+# is an MFMA, so every wait around the asm MFMAs of fa_fwd_w4 is the kernel author's. The rules, with
+# the counts hipcc itself inserts for the same pairs on gfx950 when the MFMA is a builtin (probed with
+# hipcc 7.2 --offload-arch=gfx950, scripts/microbench/mfma_hazard_probe.hip):
+#   R1  VALU write of a VGPR / AGPR  -> asm MFMA reads it as SrcA or SrcB        >= 1 wait state
+#   R2  VALU write                   -> asm MFMA reads it as SrcC                >= 2
+#   R3  asm MFMA writes a register   -> a non-MFMA instruction reads it          >= passes + 4
+#                                       (VALU, v_accvgpr_read, LDS / VMEM data)   (12 for 32x32x16, 8 for
+#                                                                                  16x16x32)
+#   R4  asm MFMA writes a register   -> another MFMA reads it as SrcA / SrcB     >= passes + 4
+#   (an MFMA reading as SrcC exactly the previous MFMA's destination is interlocked: 0)
+#   R5  an asm MFMA reads an AGPR as SrcC (an accumulator) that is undefined (kernel entry) or was consumed by a
+#       v_accvgpr_read (the epilogue's O read-out) and not written since, on some path: the stale
+#       accumulator of a previous Q block (a logic error, not a wait state; the round-3 "O zeroing by
+#       C = 0 MFMAs" build failed this way -- DESIGN.md section 5)
+# A wait state is one issue slot: an instruction counts 1, s_nop N counts N + 1, and an MFMA that
+# follows another within its pipeline occupancy first stalls until the pipe frees (passes - 1 slots
+# after the previous MFMA's issue), which the walk adds as elapsed time (back-to-back 32x32x16 MFMAs
+# issue 8 slots apart, MI355X_MICROARCH 'back-to-back issue'). The walk is a dataflow over the basic
+# blocks of the kernel (the minimum elapsed time since each register's last write over every path),
+# so a write before a branch and a read after the join are paired too.
+_INSN = re.compile(r"^\s+([a-z_][a-z0-9_]*)(?:\s+(.*))?$")
+_OPREG = re.compile(r"\b([va])\[(\d+):(\d+)\]|\b([va])(\d+)\b")
+_BRANCH = re.compile(r"^s_(cbranch_\w+|branch)$")
+_STORE = re.compile(r"^(ds_write|ds_store|buffer_store|global_store|flat_store|scratch_store)")
+_LOAD = re.compile(r"^(ds_read|ds_load|buffer_load|global_load|flat_load|scratch_load)")
+HORIZON = 40  # wait states after which no rule applies any more
+
+
+def _regs(op: str):
+    out = []
+    for m in _OPREG.finditer(op):
+        if m.group(1):
+            out += [(m.group(1), r) for r in range(int(m.group(2)), int(m.group(3)) + 1)]
+        else:
+            out.append((m.group(4), int(m.group(5))))
+    return out
+
+
+def _passes(mn: str) -> int:
+    return 8 if "32x32" in mn else 4 if "16x16" in mn else 16
+
+
+def _parse(text: str):
+    """{kernel: [(label | None, mnemonic, operand strings, in_asm, line)]} of the fa_fwd_w4 kernels."""
+    kernels, fn, in_asm = {}, None, False
+    for ln in text.splitlines():
+        m = re.match(r"^(_Z\S*):", ln)
+        if m:
+            fn = m.group(1) if m.group(1).startswith("_ZN2fa9fa_fwd_w4") else None
+            if fn:
+                kernels[fn] = []
+            continue
+        if fn is None:
+            continue
+        if ";;#ASMSTART" in ln:
+            in_asm = True
+            continue
+        if ";;#ASMEND" in ln:
+            in_asm = False
+            continue
+        lab = re.match(r"^(\.?L\w+):", ln)
+        if lab:
+            kernels[fn].append((lab.group(1), None, [], in_asm, ln))
+            continue
+        code = ln.split(";")[0]
+        im = _INSN.match(code)
+        if not im or im.group(1).startswith("."):
+            continue
+        if im.group(1) == "s_endpgm":
+            kernels[fn].append((None, "s_endpgm", [], in_asm, ln))
+            fn = None
+            continue
+        ops = [o.strip() for o in (im.group(2) or "").split(",")]
+        kernels[fn].append((None, im.group(1), ops, in_asm, ln))
+    return kernels
+
+
+def _blocks(insns):
+    """Basic blocks: [(label, [insn]), ...] and successor label lists."""
+    blocks, cur, lab = [], [], None
+    for it in insns:
+        if it[0] is not None:  # label
+            if cur or lab is not None:
+                blocks.append((lab, cur))
+            lab, cur = it[0], []
+            continue
+        cur.append(it)
+        if _BRANCH.match(it[1]) or it[1] == "s_endpgm":
+            blocks.append((lab, cur))
+            lab, cur = None, []
+    if cur or lab is not None:
+        blocks.append((lab, cur))
+    index = {lab: i for i, (lab, _) in enumerate(blocks) if lab is not None}
+    succ = []
+    for i, (_, body) in enumerate(blocks):
+        s = []
+        last = body[-1][1] if body else None
+        if last and _BRANCH.match(last):
+            tgt = body[-1][2][0] if body[-1][2] else None
+            if tgt in index:
+                s.append(index[tgt])
+            if last != "s_branch" and i + 1 < len(blocks):
+                s.append(i + 1)
+        elif last != "s_endpgm" and i + 1 < len(blocks):
+            s.append(i + 1)
+        succ.append(s)
+    return blocks, succ
+
+
+def _classify(mn, ops):
+    """(kind, dst regs, srcA, srcB, srcC, other sources) of one instruction."""
+    if mn.startswith(("v_mfma", "v_smfmac")):
+        r = [_regs(o) for o in ops[:4]] + [[]] * 4
+        return "mfma", r[0], r[1], r[2], r[3], []
+    all_regs = [_regs(o) for o in ops]
+    if _STORE.match(mn):
+        return "mem", [], [], [], [], [x for rs in all_regs for x in rs]
+    if _LOAD.match(mn):
+        dst = [] if ops and ops[-1] == "lds" or "lds" in ops else (all_regs[0] if all_regs else [])
+        return "load", dst, [], [], [], [x for rs in all_regs[1:] for x in rs]
+    if mn.startswith("v_"):
+        dst = all_regs[0] if all_regs and not mn.startswith(("v_cmp", "v_readlane", "v_readfirstlane")) else []
+        return "valu", dst, [], [], [], [x for rs in all_regs[1:] for x in rs]
+    return "other", [], [], [], [], []
+
+
+def hazards(text: str) -> list[str]:
+    """Violations of R1-R4 around the inline-asm MFMAs of every fa_fwd_w4 kernel in ``text``."""
+    out = []
+    for fn, insns in _parse(text).items():
+        blocks, succ = _blocks(insns)
+        if not blocks:
+            continue
+        # state: valu[reg] = slots since its last VALU write; mf[reg] = (slots since an asm MFMA wrote
+        # it, required); pipe = slots until the MFMA pipe is free
+        entry = [None] * len(blocks)
+        entry[0] = ({}, {}, 0, frozenset(("a", r) for r in range(256)))
+        work = [0]
+        seen_err = set()
+        while work:
+            bi = work.pop()
+            valu, mf, pipe = (dict(entry[bi][0]), dict(entry[bi][1]), entry[bi][2])
+            stale = set(entry[bi][3])
+
+            def advance(n):
+                nonlocal pipe
+                for d in (valu,):
+                    for k in list(d):
+                        d[k] += n
+                        if d[k] > HORIZON:
+                            del d[k]
+                for k in list(mf):
+                    t, req = mf[k]
+                    if t + n > HORIZON:
+                        del mf[k]
+                    else:
+                        mf[k] = (t + n, req)
+                pipe = max(0, pipe - n)
+
+            for _, mn, ops, in_asm, ln in blocks[bi][1]:
+                kind, dst, sa, sb, sc, srcs = _classify(mn, ops)
+                if kind == "mfma":
+                    advance(pipe)  # stall until the pipe accepts it
+                    if in_asm:
+                        for reg in sa + sb:
+                            if valu.get(reg, HORIZON + 1) < 1:
+                                seen_err.add(f"{fn}: R1 VALU write of {reg[0]}{reg[1]} -> asm MFMA SrcA/B with "
+                                             f"{valu[reg]} wait states (>= 1): {ln.strip()}")
+                        for reg in sc:
+                            if valu.get(reg, HORIZON + 1) < 2:
+                                seen_err.add(f"{fn}: R2 VALU write of {reg[0]}{reg[1]} -> asm MFMA SrcC with "
+                                             f"{valu[reg]} wait states (>= 2): {ln.strip()}")
+                    if in_asm:
+                        for reg in sc:  # (accumulators; operand AGPRs -- the Q fragments -- are written on
+                            # paths a path-insensitive walk cannot pair: the first block vs the next ones)
+                            if reg in stale:
+                                seen_err.add(f"{fn}: R5 asm MFMA reads {reg[0]}{reg[1]}, undefined or consumed by "
+                                             f"v_accvgpr_read on some path: {ln.strip()}")
+                    for reg in sa + sb:
+                        if reg in mf and mf[reg][0] < mf[reg][1]:
+                            seen_err.add(f"{fn}: R4 asm MFMA write of {reg[0]}{reg[1]} -> MFMA SrcA/B after "
+                                         f"{mf[reg][0]} wait states (>= {mf[reg][1]}): {ln.strip()}")
+                    advance(1)
+                    pipe = _passes(mn) - 1
+                    for reg in dst:
+                        stale.discard(reg)
+                        valu.pop(reg, None)
+                        if in_asm:
+                            mf[reg] = (0, _passes(mn) + 4)
+                        else:
+                            mf.pop(reg, None)
+                    continue
+                for reg in srcs:
+                    if reg in mf and mf[reg][0] < mf[reg][1]:
+                        seen_err.add(f"{fn}: R3 asm MFMA write of {reg[0]}{reg[1]} -> {mn} after {mf[reg][0]} "
+                                     f"wait states (>= {mf[reg][1]}): {ln.strip()}")
+                nop = re.match(r"s_nop", mn)
+                advance(int(ops[0], 0) + 1 if nop and ops and ops[0] else 1)
+                if mn.startswith("v_accvgpr_read"):
+                    stale.update(r for r in srcs if r[0] == "a")
+                for reg in dst:
+                    stale.discard(reg)
+                    mf.pop(reg, None)
+                    if kind == "valu":
+                        valu[reg] = 0
+                    else:
+                        valu.pop(reg, None)
+            for s in succ[bi]:
+                if entry[s] is None:
+                    entry[s] = ({k: v for k, v in valu.items()}, dict(mf), pipe, frozenset(stale))
+                    work.append(s)
+                    continue
+                ov, om, op_, ost = entry[s]
+                nv = dict(ov)
+                for k, v in valu.items():
+                    nv[k] = min(v, nv.get(k, HORIZON + 1))
+                nm = dict(om)
+                for k, (t, req) in mf.items():
+                    if k not in nm or t < nm[k][0]:
+                        nm[k] = (t, max(req, nm.get(k, (0, 0))[1]))
+                npipe = min(op_, pipe)  # (the smaller stall: elapsed time is a lower bound)
+                nst = ost | frozenset(stale)
+                if (nv, nm, npipe, nst) != (ov, om, op_, ost):
+                    entry[s] = (nv, nm, npipe, nst)
+                    work.append(s)
+        out += sorted(seen_err)
+    return out
+
+
 def check_file(path) -> list[str]:
     text = open(path).read()
     if "fa_fwd_w4" not in text:
         return [f"{path}: no fa_fwd_w4 kernel in the assembly (stale or wrong file)"]
-    return agpr_violations(text) + spills(text)
+    return agpr_violations(text) + spills(text) + hazards(text)
 
 
 if __name__ == "__main__":

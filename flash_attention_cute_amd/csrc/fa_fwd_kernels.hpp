@@ -574,6 +574,16 @@ __device__ __forceinline__ void agpr_mfma(const u32x4 &a, const u32x4 &b) {
     FA_CASE(0) FA_CASE(16) FA_CASE(32) FA_CASE(48) FA_CASE(64) FA_CASE(80) FA_CASE(96) FA_CASE(112)
 #undef FA_CASE
 }
+#ifdef FA_EXP_CZERO
+// (experiment only) a[BASE..BASE+15] = A.B with C = 0
+template <bool kF16, int BASE>
+__device__ __forceinline__ void agpr_mfma_c0(const u32x4 &a, const u32x4 &b) {
+    if constexpr (kF16)
+        asm volatile("v_mfma_f32_32x32x16_f16 a[%2:%3], %0, %1, 0" ::"v"(a), "v"(b), "n"(BASE), "n"(BASE + 15) : "memory");
+    else
+        asm volatile("v_mfma_f32_32x32x16_bf16 a[%2:%3], %0, %1, 0" ::"v"(a), "v"(b), "n"(BASE), "n"(BASE + 15) : "memory");
+}
+#endif
 template <int DTL, bool kBlockB>
 __device__ __forceinline__ void agpr_scale(const float alpha) {
     if constexpr (DTL == 4) {
@@ -1360,7 +1370,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     }(), "phase-2 softmax schedule");
     // AD: bit 0 = block A has no visible score in tile cs (its early softmax units are skipped),
     // bit 1 = nor in tile cp (its P.V MFMAs are skipped: P is 0)
-    auto phase2 = [&](const char *V, auto PPV, auto PSM, auto SM1, auto AD) __attribute__((always_inline)) {
+    auto phase2 = [&](const char *V, auto PPV, auto PSM, auto SM1, auto AD, const bool czf = false)
+        __attribute__((always_inline)) {
+        (void)czf;
         constexpr int cp = decltype(PPV)::value, cs = decltype(PSM)::value;
         constexpr bool do_sm = decltype(SM1)::value;
         constexpr bool sdead = decltype(AD)::value & 1, pdead = decltype(AD)::value & 2;
@@ -1387,7 +1399,14 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #ifndef FA_EXP_NOLGKM2
             if constexpr (kk > 0 && i == 0) __builtin_amdgcn_s_waitcnt(kLgkm0);
 #endif
+#ifdef FA_EXP_CZERO
+            if constexpr (!(pdead && X == 0)) {
+                if (kk == 0 && czf) agpr_mfma_c0<F, X * 16 * DTL + 16 * dt>(va[kk & 1][dt], P[cp][4 * X + kk]);
+                else agpr_mfma<F, X * 16 * DTL + 16 * dt, true>(va[kk & 1][dt], P[cp][4 * X + kk]);
+            }
+#else
             if constexpr (!(pdead && X == 0)) agpr_mfma<F, X * 16 * DTL + 16 * dt, true>(va[kk & 1][dt], P[cp][4 * X + kk]);
+#endif
             FA_SCHED_FENCE();  // (see phase 1)
             if constexpr (kk + 1 < 4 && i < DTL) {
 #if defined(FA_EXP_HALFLDS) || defined(FA_EXP_HALFV)  // (timing experiment, as in phase 1: half the V^T reads)
@@ -1490,7 +1509,15 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     for (int X = 0; X < 2; ++X) {
         st[X] = {kNeg, 0.f, 1.f, kNeg + thr_raw, kNeg, kNeg, 0.f, 0.f, 0ull};
     }
+#ifdef FA_EXP_CZERO
+    // (round-3 experiment rebuilt for the analysis in DESIGN.md: no O zeroing here; the block's first
+    // UNMASKED iteration writes O with C = 0 P.V MFMAs instead -- a block whose first iteration is a
+    // masked one (causal first q-tiles, windows) then accumulates into the previous block's O. Gate:
+    // _asm_check rule R5 rejects this build.)
+    bool cz_first = true;
+#else
     if constexpr (DTL == 4) fa_agpr_zero_4(); else fa_agpr_zero_2();
+#endif
     // tile -1 of the pipeline is empty: its S = kNeg gives P = 0, and its P.V reads V slot 1,
     // zeroed here so that 0 * V stays 0 (the previous block's V may hold non-finite values).
 #pragma unroll
@@ -1593,7 +1620,12 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #if defined(FA_EXP_NOSM)
         phase2(lds + KV0 + (2 + pr) * T, IC<pr>{}, PAR, IC<0>{}, AD{});
 #else
+#ifdef FA_EXP_CZERO
+        phase2(lds + KV0 + (2 + pr) * T, IC<pr>{}, PAR, IC<1>{}, AD{}, mk == 0 && cz_first);
+        if constexpr (mk == 0) cz_first = false;
+#else
         phase2(lds + KV0 + (2 + pr) * T, IC<pr>{}, PAR, IC<1>{}, AD{});
+#endif
 #endif
         rescale(j == j_lo);
         FA_STAMP(sc_);

@@ -380,3 +380,50 @@ def test_host_validation_under_asan_ubsan(tmp_path):
     res = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=120)
     assert res.returncode == 0 and "abi validation ok" in res.stdout, res.stdout + res.stderr
     assert "runtime error" not in res.stderr and "AddressSanitizer" not in res.stderr, res.stderr
+
+
+def test_mfma_hazard_rules_on_synthetic_streams():
+    """_asm_check.hazards (the build gate around fa_fwd_w4's inline-asm MFMAs): each rule fires on a
+    minimal stream and stays quiet once the wait states the gfx950 compiler itself inserts for the
+    same pair are there (R1 1, R2 2, R3 passes + 4 = 12 for 32x32x16)."""
+    from flash_attention_cute_amd import _asm_check as A
+
+    k = "_ZN2fa9fa_fwd_w4ITEST:\n"
+
+    def run(body):
+        return A.hazards(k + body + "\ts_endpgm\n")
+
+    asm = lambda ins: f"\t;;#ASMSTART\n\t{ins}\n\t;;#ASMEND\n"  # noqa: E731
+    mf = "v_mfma_f32_32x32x16_f16"
+    r1 = "\tv_mov_b32_e32 v4, 0\n" + asm(f"{mf} a[0:15], v[4:7], v[8:11], 0")
+    assert [h.split(": ")[1][:2] for h in run(r1)] == ["R1"]
+    assert run("\tv_mov_b32_e32 v4, 0\n\ts_nop 0\n" + asm(f"{mf} a[0:15], v[4:7], v[8:11], 0")) == []
+    zero16 = "".join(f"\tv_accvgpr_write_b32 a{i}, 0\n" for i in range(16))
+    r2 = zero16 + "\ts_nop 0\n" + asm(f"{mf} a[0:15], v[4:7], v[8:11], a[0:15]")
+    assert [h.split(": ")[1][:2] for h in run(r2)] == ["R2"]
+    assert run(r2.replace("s_nop 0", "s_nop 1")) == []
+    r3 = asm(f"{mf} v[0:15], v[20:23], v[24:27], 0") + "\ts_nop 3\n\tv_add_f32_e32 v30, v1, v2\n"
+    assert {h.split(": ")[1][:2] for h in run(r3)} == {"R3"}
+    assert run(asm(f"{mf} v[0:15], v[20:23], v[24:27], 0") + "\ts_nop 11\n\tv_add_f32_e32 v30, v1, v2\n") == []
+    # back-to-back MFMAs issue 8 slots apart (the pipe): three of them cover the 12 wait states
+    three = asm(f"{mf} v[0:15], v[20:23], v[24:27], 0\n\t{mf} v[40:55], v[20:23], v[24:27], 0\n\t"
+                f"{mf} v[60:75], v[20:23], v[24:27], 0")
+    assert run(three + "\tv_add_f32_e32 v30, v1, v2\n") == []
+    # R5: an accumulator read out (epilogue) and accumulated into again without a re-zeroing write
+    z = "".join(f"\tv_accvgpr_write_b32 a{i}, 0\n" for i in range(16)) + "\ts_nop 1\n"
+    body = z + asm(f"{mf} a[0:15], v[4:7], v[8:11], a[0:15]") + "\ts_nop 15\n\tv_accvgpr_read_b32 v50, a0\n"
+    loop = ".LBB0_1:\n" + body + "\ts_cbranch_scc1 .LBB0_1\n"
+    assert any("R5" in h for h in run(loop.replace(z, "")))  # never zeroed: undefined, then stale
+    assert run(loop) == []
+
+
+def test_mfma_hazard_gate_passes_the_product_assembly():
+    from flash_attention_cute_amd import _asm_check as A
+    from flash_attention_cute_amd import _build
+
+    files = sorted((_build.ROOT / "build" / "obj").glob("*/fa_inst-hip-amdgcn-amd-amdhsa-gfx950.s"))
+    if not files:
+        pytest.skip("no product assembly in build/obj (run __graft_entry__.build())")
+    assert len(files) == 16
+    for f in files:
+        assert A.hazards(f.read_text()) == [], f
