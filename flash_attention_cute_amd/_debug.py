@@ -50,6 +50,9 @@ def lib(debug: bool = False) -> ctypes.CDLL:
         lib.fa_debug_set_knobs.restype = None
         lib.fa_debug_last_path.restype = ctypes.c_int
         lib.fa_last_error.restype = ctypes.c_char_p
+        lib.fa_debug_set_zigzag.argtypes = [ctypes.c_int]
+        lib.fa_debug_set_zigzag.restype = None
+        lib.fa_debug_last_zigzag.restype = ctypes.c_int
         _libs[debug] = lib
     return _libs[debug]
 
@@ -80,6 +83,17 @@ def knobs(debug: bool = False, **kw):
 def last_path(debug: bool = False) -> str:
     """Kernel the last call on this thread launched ("w4", "decode_split", ...)."""
     return PATHS.get(lib(debug).fa_debug_last_path(), "unknown")
+
+
+def set_zigzag(mode: int | None = None, debug: bool = False) -> None:
+    """Causal Q-block layout of fa_fwd_w4: 0 never zigzag, 1 when the blocks fit one round of the
+    persistent grid (the default), 2 always where it applies; None restores the default."""
+    lib(debug).fa_debug_set_zigzag(-1 if mode is None else int(mode))
+
+
+def last_zigzag(debug: bool = False) -> bool:
+    """Whether the last prefill launch on this thread ran zigzag Q blocks."""
+    return bool(lib(debug).fa_debug_last_zigzag())
 
 
 def forward(q, k, v, softmax_scale=None, causal=False, variant="w8", window_left=-1, w4_grid=None):

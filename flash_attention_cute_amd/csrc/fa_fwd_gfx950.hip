@@ -35,13 +35,14 @@ unsigned long long *g_stamps = nullptr;
 thread_local int g_last_path = fa::kPathNone;
 
 fa::Knobs knobs_from_env() {
-    fa::Knobs k{0, 0, 1, fa::kDecTargetWgs, fa::kDecNt};
+    fa::Knobs k{0, 0, 1, fa::kDecTargetWgs, fa::kDecNt, 1};
     if (const char *v = getenv("FA_GFX950_VARIANT"))
         k.variant = !strcmp(v, "w8") ? 1 : !strcmp(v, "w4slow") ? 2 : !strcmp(v, "p8") ? 3 : 0;
     if (const char *e = getenv("FA_W4_GRID")) k.w4_grid = atoll(e) > 0 ? atoll(e) : 0;
     if (const char *e = getenv("FA_GFX950_DECODE")) k.decode = strcmp(e, "0") != 0;
     if (const char *e = getenv("FA_DEC_TARGET_WGS")) k.dec_target = atoll(e) > 0 ? atoll(e) : fa::kDecTargetWgs;
     if (const char *e = getenv("FA_DEC_FLAGS")) k.dec_flags = atoi(e);
+    if (const char *e = getenv("FA_ZIGZAG")) k.zigzag = atoi(e);
 #ifdef FA_DEBUG_VARIANTS
     if (k.variant != 0)  // a debug / A-B body replaces the product kernel for the whole process: say so
         fprintf(stderr,
@@ -91,10 +92,20 @@ extern "C" void fa_debug_set_knobs(int variant, int64_t w4_grid, int decode, int
     k.dec_flags = dec_flags < 0 ? d.dec_flags : dec_flags;
 }
 extern "C" int fa_debug_last_path(void) { return g_last_path; }
+// zigzag knob (fa_launch.h Knobs::zigzag): 0 never, 1 when the blocks fit one round, 2 always; < 0
+// restores the environment / default value. Whether the last prefill launch ran zigzag blocks.
+extern "C" void fa_debug_set_zigzag(int mode) {
+    knobs_mut().zigzag = mode < 0 ? env_defaults().zigzag : mode;
+}
+namespace {
+thread_local int g_last_zigzag = 0;
+}
+extern "C" int fa_debug_last_zigzag(void) { return g_last_zigzag; }
+void fa::set_last_zigzag(int z) { g_last_zigzag = z; }
 
 unsigned long long *fa::stamp_buffer() { return g_stamps; }
 
-int64_t fa::w4_grid(int64_t nwg) {
+int64_t fa::device_cus() {
     // CU count per device, queried once (a racing first query writes the same value)
     static int cus[64] = {0};
     int dev = 0;
@@ -105,7 +116,11 @@ int64_t fa::w4_grid(int64_t nwg) {
             n = 256;
         if (dev >= 0) cus[dev] = n;
     }
-    int64_t cap = n;
+    return n;
+}
+
+int64_t fa::w4_grid(int64_t nwg) {
+    int64_t cap = device_cus();
     if (fa::knobs().w4_grid > 0) cap = fa::knobs().w4_grid;
     if (nwg <= cap) return nwg;  // one Q block per workgroup
     // Capped: the kernel deals Q block i to the workgroups with (bid & 7) == (i & 7), so every
@@ -450,7 +465,6 @@ extern "C" int fa_abi_version(void) { return FA_GFX950_ABI_VERSION; }
 
 extern "C" int fa_fwd_gfx950_geometry(const fa_fwd_params *params, int causal, int64_t *block_m,
                                       int64_t *block_n, int64_t *threads, int64_t *workgroups) {
-    (void)causal;
     if (!params) return set_err(FA_ERR_INVALID_ARGUMENT, "params is NULL");
     if (use_decode(*params)) {
         // without a workspace fa_fwd_gfx950 runs the decode kernel unsplit
@@ -461,7 +475,8 @@ extern "C" int fa_fwd_gfx950_geometry(const fa_fwd_params *params, int causal, i
         if (workgroups) *workgroups = fa::decode_units(*params, a) * a.n_split;
         return FA_OK;
     }
-    const int64_t n_qtiles = (params->seqlen_q + fa::kBlockM - 1) / fa::kBlockM;
+    const int64_t n_qtiles = fa::use_zigzag(*params, causal != 0, kNoPath) ? fa::zigzag_qtiles(params->seqlen_q)
+                                                                          : (params->seqlen_q + fa::kBlockM - 1) / fa::kBlockM;
     if (block_m) *block_m = fa::kBlockM;
     if (block_n) *block_n = fa::kBlockN;
     if (threads) *threads = (fa::variant_from_env() == 1 || fa::variant_from_env() == 3 ? fa::kThreads : 256);

@@ -914,6 +914,25 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     uint32_t rnd = 0, kblk = block_of(0);
     if (kblk >= cnt) return;
 
+    // Zigzag Q blocks (xa.zigzag, dense causal launches whose blocks fit one round of the grid):
+    // block t pairs the 128-row segment t (block A) with segment nseg - 1 - t (block B), so every
+    // block carries the same causal work -- a short top segment and a long bottom one -- instead of
+    // the heaviest of the 256-row blocks setting the span (the C4 rank share at N = 8: 256 blocks on
+    // 256 CUs). Block A's rows are always the workgroup's first 128 rows from m0 (the A-dead tiles
+    // below follow); block B's rows start rowB rows after block A's (128 for the plain layout).
+    const bool zz = kCausal && xa.zigzag;
+    auto geom_of = [&](const int qtile, const int sq, int &m0o, int &rowbo) __attribute__((always_inline)) {
+        if (zz) {
+            const int nseg = (sq + 127) >> 7, sB = nseg - 1 - qtile;
+            m0o = qtile << 7;
+            rowbo = sB > qtile ? (sB - qtile) << 7 : (nseg - qtile) << 7;  // (no partner: rows past Sq)
+        } else {
+            m0o = qtile * kBlockM;
+            rowbo = kRowB;
+        }
+    };
+    int rowB = kRowB, rowB_next = kRowB;
+
     // per-block geometry (set_block)
     const char *qb, *kb, *vb;
     const char *cosb = nullptr, *sinb = nullptr;  // RoPE tables of this block's sequence (xa.cos)
@@ -949,14 +968,16 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         kb = (const char *)p.k_ptr + 2 * (krow0 + (int64_t)hkv * p.k_head_stride);
         vb = (const char *)p.v_ptr + 2 * (vrow0 + (int64_t)hkv * p.v_head_stride);
         ob = (char *)p.o_ptr + 2 * (orow0 + (int64_t)hq * p.o_head_stride);
-        m0 = wk.qtile * kBlockM;
+        geom_of(wk.qtile, Sq, m0, rowB);
         // rows interleaved over the waves: block A = rows mw..mw+31 (the workgroup's first half),
-        // block B = rows mw+kRowB.. (its second half), so the last causal diagonal tiles hold no
+        // block B = rows mw+rowB.. (its second half), so the last causal diagonal tiles hold no
         // score of any wave's block A (A-dead tiles, below)
         mw = m0 + wave * 32;
         n_end = n_blocks;
         if (kCausal) {
-            const int x = diag + min(m0 + kBlockM, Sq);
+            // the workgroup's last row: block B's (zigzag: block A's when B has no partner segment)
+            const int last = min(m0 + rowB < Sq ? m0 + rowB + kRowB : m0 + kRowB, Sq);
+            const int x = diag + (zz ? last : min(m0 + kBlockM, Sq));
             const int nb = x <= 0 ? 0 : (x + kBlockN - 1) / kBlockN;
             n_end = min(nb, n_blocks);
         }
@@ -980,14 +1001,14 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     set_block(decode_work<kCausal>(nwg, xcd + 8 * kblk, n_qtiles, (int)p.num_heads_q, (int)p.head_q_per_group));
 
     // ---- Q: this wave's 64 rows, B-operand fragments straight from HBM into AGPRs ----------
-    // lane (h, r) of block X holds Q[mw + kRowB*X + r][16*ks + 8*h + 0..7]; rows >= Sq read as 0.
+    // lane (h, r) of block X holds Q[mw + rowB*X + r][16*ks + 8*h + 0..7]; rows >= Sq read as 0.
     // Asynchronous: retired by the vmcnt wait ahead of the block's first barrier.
     auto load_q = [&]() __attribute__((always_inline)) {
         const int qs = (int)p.q_seqlen_stride;
-        const rsrc_t qr = make_rsrc(qb + 2 * (int64_t)mw * qs, slab_bytes(min(Sq - mw, kRowSpan), qs, D));
+        const rsrc_t qr = make_rsrc(qb + 2 * (int64_t)mw * qs, slab_bytes(min(Sq - mw, rowB + 32), qs, D));
         auto qoff = [&](const int X, const int ks) {
             const bool ok = kExactD || 16 * ks + 8 * h < D;  // columns past D read as 0
-            return ok ? (kRowB * X + r) * qs * 2 + 32 * ks + 16 * h : 0x7ffffff0;
+            return ok ? (rowB * X + r) * qs * 2 + 32 * ks + 16 * h : 0x7ffffff0;
         };
         static_for<2 * KS>([&](auto I) {
             constexpr int i = decltype(I)::value;
@@ -1001,7 +1022,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     const bool rope_q = kExactD && xa.cos != nullptr;
     auto load_q_rope = [&]() __attribute__((always_inline)) {
         const int qs = (int)p.q_seqlen_stride, cs = (int)xa.seq_stride;
-        const int rows = min(Sq - mw, kRowSpan);
+        const int rows = min(Sq - mw, rowB + 32);
         const rsrc_t qr = make_rsrc(qb + 2 * (int64_t)mw * qs, slab_bytes(rows, qs, D));
         const rsrc_t cr = make_rsrc(cosb + 2 * (int64_t)mw * cs, slab_bytes(rows, cs, D));
         const rsrc_t sr = make_rsrc(sinb + 2 * (int64_t)mw * cs, slab_bytes(rows, cs, D));
@@ -1010,9 +1031,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             u32x4 qv[KS], cv[KS], sv[KS];
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
-                qv[ks] = __builtin_amdgcn_raw_buffer_load_b128(qr, (kRowB * X + r) * qs * 2 + 32 * ks + 16 * h, 0, 0);
-                cv[ks] = __builtin_amdgcn_raw_buffer_load_b128(cr, (kRowB * X + r) * cs * 2 + 32 * ks + 16 * h, 0, 0);
-                sv[ks] = __builtin_amdgcn_raw_buffer_load_b128(sr, (kRowB * X + r) * cs * 2 + 32 * ks + 16 * h, 0, 0);
+                qv[ks] = __builtin_amdgcn_raw_buffer_load_b128(qr, (rowB * X + r) * qs * 2 + 32 * ks + 16 * h, 0, 0);
+                cv[ks] = __builtin_amdgcn_raw_buffer_load_b128(cr, (rowB * X + r) * cs * 2 + 32 * ks + 16 * h, 0, 0);
+                sv[ks] = __builtin_amdgcn_raw_buffer_load_b128(sr, (rowB * X + r) * cs * 2 + 32 * ks + 16 * h, 0, 0);
             }
             static_for<KS>([&](auto KK) {
                 constexpr int ks = decltype(KK)::value;
@@ -1030,16 +1051,17 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     const int q_ch0 = G::k_off(q_row_l, ((16 * lane) % RB) / 16) % RB / 16;
     const uint32_t q_lane_off = (uint32_t)(q_row_l * qs_ * 2);
     const uint32_t q_lds = lds_u32(lds) + QOFF + wave * T;  // this wave's Q image
-    auto q_piece = [&](const rsrc_t &qr, const int n) __attribute__((always_inline)) {
+    auto q_piece = [&](const rsrc_t &qr, const int n, const int rb) __attribute__((always_inline)) {
         const int ch = q_ch0 ^ (4 * (n & (RB == 256 ? 3 : 1)));
-        // image rows 0..31 are block A's rows mw.., rows 32..63 block B's rows mw+kRowB..
-        const int srow = n * ROWS_PER_PIECE + (n >= NQP / 2 ? kRowB - 32 : 0);
+        // image rows 0..31 are block A's rows mw.., rows 32..63 block B's rows mw+rb.. (rb: that
+        // block's rowB)
+        const int srow = n * ROWS_PER_PIECE + (n >= NQP / 2 ? rb - 32 : 0);
         uint32_t voff = q_lane_off + (uint32_t)(srow * qs_ * 2) + 16u * (uint32_t)ch;
         if (!kExactD && ch * 8 >= D) voff = 0x7ffffff0u;  // columns past D read as 0
         dma_one(qr, q_lds + n * 1024, (int)voff, true);
     };
-    // this wave's Q slab of block wk (rows past the sequence read as 0)
-    auto q_rsrc_of = [&](const Work wk) __attribute__((always_inline)) {
+    // this wave's Q slab of block wk (rows past the sequence read as 0); rb: that block's rowB
+    auto q_rsrc_of = [&](const Work wk, int &rb) __attribute__((always_inline)) {
         int64_t row0 = (int64_t)wk.b * p.q_batch_stride;
         int sq = (int)p.seqlen_q;
         if (xa.q_rng) {
@@ -1047,9 +1069,11 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             sq = xa.q_rng[wk.b + xa.rng_hi] - q0;
             row0 = (int64_t)q0 * qs_;
         }
-        const int mwn = wk.qtile * kBlockM + wave * 32;
+        int m0n;
+        geom_of(wk.qtile, sq, m0n, rb);
+        const int mwn = m0n + wave * 32;
         const char *qbn = (const char *)p.q_ptr + 2 * (row0 + (int64_t)wk.hq * p.q_head_stride);
-        return make_rsrc_u(qbn + 2 * (int64_t)mwn * qs_, slab_bytes(min(sq - mwn, kRowSpan), qs_, D));
+        return make_rsrc_u(qbn + 2 * (int64_t)mwn * qs_, slab_bytes(min(sq - mwn, rb + 32), qs_, D));
     };
     // the next block (decoded once, in this block's prologue) and its Q pieces: qn of qnt issued
     // (kQL == 2: during this block's tiles)
@@ -1063,15 +1087,16 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         if (kn < cnt) {
             wk_next = decode_work<kCausal>(nwg, xcd + 8 * kn, n_qtiles, (int)p.num_heads_q, (int)p.head_q_per_group);
             if (kQL && !rope_q) {
-                qnr = q_rsrc_of(wk_next);
+                qnr = q_rsrc_of(wk_next, rowB_next);
                 qnt = NQP;
             }
         }
     };
     if (!rope_q) {
         if constexpr (kQL != 0) {
-            const rsrc_t qr0 = q_rsrc_of(decode_work<kCausal>(nwg, xcd + 8 * kblk, n_qtiles, (int)p.num_heads_q, (int)p.head_q_per_group));
-            static_for<NQP>([&](auto N) { q_piece(qr0, decltype(N)::value); });
+            int rb0;
+            const rsrc_t qr0 = q_rsrc_of(decode_work<kCausal>(nwg, xcd + 8 * kblk, n_qtiles, (int)p.num_heads_q, (int)p.head_q_per_group), rb0);
+            static_for<NQP>([&](auto N) { q_piece(qr0, decltype(N)::value, rb0); });
         } else {
             load_q();
         }
@@ -1304,7 +1329,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             // the next block's Q: kQPT pieces per tile, in evenly spaced gaps
             if constexpr (kQL == 2 && kQPhase == 1 && do_dma && i == 3 && (ks * kQPT) % KS == 0) {
                 if (qn < qnt) {
-                    q_piece(qnr, qn);
+                    q_piece(qnr, qn, rowB_next);
                     ++qn;
                 }
             }
@@ -1439,7 +1464,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             // (kQPhase 2) the next block's Q pieces early in phase 2, where no K/V DMA is issued
             if constexpr (kQL == 2 && kQPhase == 2 && do_sm && g % 2 == 1 && g < 2 * kQPT) {
                 if (__builtin_expect(qn < qnt, 0)) {  // (out of line: the common path falls through)
-                    q_piece(qnr, qn);
+                    q_piece(qnr, qn, rowB_next);
                     ++qn;
                 }
             }
@@ -1623,9 +1648,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                     mask(S[c][0], S[c][1], mw, key0);
                 }
             }
-            if (hides(mw + kRowB, key0)) {
+            if (hides(mw + rowB, key0)) {
                 s_ready(S[c][2], S[c][3]);
-                mask(S[c][2], S[c][3], mw + kRowB, key0);
+                mask(S[c][2], S[c][3], mw + rowB, key0);
             }
         }
 #endif
@@ -1689,7 +1714,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // workgroup's first half, m0 .. m0 + kRowB - 1): they run B only (MASKED 2, then 3)
     int jA = n_loop;
     if (kCausal) {
-        const int x = min(Sk - 1, m0 + kRowB - 1 + diag);  // the last visible key of block A
+        // the last visible key of block A (rows m0 .. m0 + 127 in both layouts)
+        const int x = min(Sk - 1, m0 + kRowB - 1 + diag);
         jA = x < 0 ? 0 : x / kBlockN + 1;
     }
     {
@@ -1733,7 +1759,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         s_ready(S[0][0], S[0][1]);
         s_ready(S[0][2], S[0][3]);
         mask(S[0][0], S[0][1], mw, key0);
-        mask(S[0][2], S[0][3], mw + kRowB, key0);
+        mask(S[0][2], S[0][3], mw + rowB, key0);
         sm1_all(IC<0>{});
         rescale(j == j_lo);
         sm2_all(IC<0>{}, IC<0>{});
@@ -1748,7 +1774,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // Every wave is past this block's last barrier: the Q AGPRs and both K slots are free (the
     // drain reads only a V slot).
     char *const ob_c = ob;
-    const int mw_c = mw, sq_c = Sq, jlo_c = j_lo;
+    const int mw_c = mw, sq_c = Sq, jlo_c = j_lo, rowb_c = rowB;
 #ifdef FA_STAMPS
     const uint32_t blk_c = xcd + 8 * kblk;
 #endif
@@ -1761,7 +1787,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         // issued here and read in the prologue
         q_in_agpr = kQL && qnt > 0 && qn == qnt;
         if constexpr (kQL != 0) {
-            for (; qn < qnt; ++qn) q_piece(qnr, qn);
+            for (; qn < qnt; ++qn) q_piece(qnr, qn, rowB_next);
         } else if (!rope_q) {
             load_q();
         }
@@ -1788,7 +1814,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // ---- epilogue ---------------------------------------------------------------------------
     mfma_drain();  // last asm MFMA -> AGPR reads
     const int os_ = (int)p.o_seqlen_stride;
-    const rsrc_t orr = make_rsrc(ob_c + 2 * (int64_t)mw_c * os_, slab_bytes(min(sq_c - mw_c, kRowSpan), os_, D));
+    const rsrc_t orr = make_rsrc(ob_c + 2 * (int64_t)mw_c * os_, slab_bytes(min(sq_c - mw_c, rowb_c + 32), os_, D));
     auto store_block = [&](const int row, auto OBASE, const float l_tot) {
         constexpr int ob0 = decltype(OBASE)::value;
         f32x16 o[DTL];
@@ -1823,7 +1849,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     const float l0 = pair_sum(st[0].l);
     const float l1 = pair_sum(st[1].l);
     store_block(r, IC<0>{}, l0);
-    store_block(r + kRowB, IC<16 * DTL>{}, l1);
+    store_block(r + rowb_c, IC<16 * DTL>{}, l1);
 #ifdef FA_STAMPS
     {
         __builtin_amdgcn_s_waitcnt(0);
@@ -1859,27 +1885,32 @@ int launch_p8(const fa_fwd_params &p, hipStream_t stream);
 template <class DT, bool C, int kD, bool kExact>
 int launch_one(const fa_fwd_params &p, const PathArgs &xa, hipStream_t stream) {
     if (xa.cos && !kExact) return set_err(FA_ERR_UNSUPPORTED, "fused RoPE needs head dim 64 or 128");
-    const int64_t n_qtiles = (p.seqlen_q + kBlockM - 1) / kBlockM;
-    const int64_t nwg = n_qtiles * p.num_heads_q * p.batch_size;
     // varlen, fused RoPE and the local window run fa_fwd_w4 (w4slow under the debug variant); w8 / p8
     // have none of them
 #ifdef FA_DEBUG_VARIANTS
     const bool w4_only = xa.k_rng || xa.cos || xa.window_left >= 0;
     const int variant = w4_only && (variant_from_env() == 1 || variant_from_env() == 3) ? 0 : variant_from_env();
     if (variant == 3) return launch_p8<DT, C, kD, kExact>(p, stream);
+#else
+    constexpr int variant = 0;  // the product library: fa_fwd_w4 only
+#endif
+    PathArgs xz = xa;  // (fa_fwd_w4 / w4slow: zigzag Q blocks for a causal launch that fits one round)
+    xz.zigzag = variant != 1 && use_zigzag(p, C, xa) ? 1 : 0;
+    const int64_t n_qtiles = xz.zigzag ? zigzag_qtiles(p.seqlen_q) : (p.seqlen_q + kBlockM - 1) / kBlockM;
+    const int64_t nwg = n_qtiles * p.num_heads_q * p.batch_size;
+#ifdef FA_DEBUG_VARIANTS
     if (variant == 1)
         hipLaunchKernelGGL((fa_fwd_w8<DT, C, kD, kExact>), dim3((uint32_t)nwg), dim3(kThreads), 0, stream, p,
                            (int)n_qtiles);
     else
-#else
-    constexpr int variant = 0;  // the product library: fa_fwd_w4 only
 #endif
         // persistent: about one workgroup per CU (the kernel walks the Q blocks itself)
         hipLaunchKernelGGL((fa_fwd_w4<DT, C, kD, kExact>), dim3((uint32_t)w4_grid(nwg)), dim3(256), 0, stream, p,
-                           (int)n_qtiles, variant == 2 ? 1 : 0, stamp_buffer(), xa);
+                           (int)n_qtiles, variant == 2 ? 1 : 0, stamp_buffer(), xz);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "HIP launch failed: %s", hipGetErrorString(e));
     set_last_path(variant == 1 ? kPathW8 : variant == 2 ? kPathW4Slow : kPathW4);
+    set_last_zigzag(xz.zigzag);
     return FA_OK;
 }
 

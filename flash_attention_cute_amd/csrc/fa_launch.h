@@ -38,19 +38,24 @@ int set_err(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3))
 //   decode     split-KV decode kernel for few rows per kv-head (FA_GFX950_DECODE=0 turns it off)
 //   dec_target workgroups the decode split plan aims at (FA_DEC_TARGET_WGS)
 //   dec_flags  kDec* bits of the decode kernel (FA_DEC_FLAGS)
+//   zigzag     causal Q-block layout: 1 = zigzag when the blocks fit one round of the persistent
+//              grid (default), 0 = never, 2 = always where it applies (FA_ZIGZAG; tests)
 struct Knobs {
     int variant;
     int64_t w4_grid;
     int decode;
     int64_t dec_target;
     int dec_flags;
+    int zigzag;
 };
+
 const Knobs &knobs();
 inline int variant_from_env() { return knobs().variant; }
 
 // Which kernel the last fa_fwd_gfx950* call on this thread launched (fa_debug_last_path)
 enum Path { kPathNone = 0, kPathW4 = 1, kPathW8 = 2, kPathW4Slow = 3, kPathDecode = 4, kPathDecodeSplit = 5, kPathP8 = 6 };
 void set_last_path(int path);
+void set_last_zigzag(int z);
 
 // diagnostic per-wave phase stamps of fa_fwd_w4 (only a -DFA_STAMPS=1 build writes them; see
 // fa_debug_set_stamps in fa_fwd_gfx950.hip and scripts/stamps.py); nullptr otherwise
@@ -60,6 +65,10 @@ unsigned long long *stamp_buffer();
 // count of the current device), else the cap rounded down to a multiple of 8, at least 8 (the kernel
 // deals Q blocks to workgroups by bid mod 8). FA_W4_GRID=<n> overrides the cap (A/B runs, tests).
 int64_t w4_grid(int64_t nwg);
+// compute units of the current device (queried once per device)
+int64_t device_cus();
+
+
 
 // Optional parts of a prefill launch.
 // RoPE tables for the Q load (fa_fwd_gfx950_rope): cos / sin [.., Sq, D] of the q dtype, strides in
@@ -76,6 +85,8 @@ int64_t w4_grid(int64_t nwg);
 // (fa_fwd_gfx950_padded). Masks are bottom-right aligned per sequence.
 // k_lo / k_hi (decode kernel only, fa_fwd_gfx950_padded): key POSITIONS [k_lo[b], k_hi[b]) within
 // batch row b (its batch strides apply), or nullptr.
+// zigzag (set by launch_one, never by the dispatchers): causal Q blocks pair the 128-row segments t
+// and nseg - 1 - t (fa_fwd_w4 "Zigzag Q blocks"), for dense causal launches that fit one round.
 struct PathArgs {
     const void *cos;
     const void *sin;
@@ -85,7 +96,21 @@ struct PathArgs {
     int rng_hi;
     const int *q_rng, *k_rng;
     const int *k_lo, *k_hi;
+    int zigzag;
 };
+
+// Whether a prefill launch runs zigzag Q blocks, and its logical q-tile count (blocks per (batch,
+// q-head)): causal, dense (no per-sequence ranges, window or RoPE), more than one 128-row segment,
+// the plain blocks fitting one round of the grid (knob 1) or always (knob 2), and the wave's Q / O
+// slab (block B up to Sq rows past block A) inside 32-bit byte offsets.
+inline bool use_zigzag(const fa_fwd_params &p, bool causal, const PathArgs &xa) {
+    if (!causal || xa.k_rng || xa.cos || xa.window_left >= 0 || knobs().zigzag == 0 || p.seqlen_q <= 128) return false;
+    const int64_t big = p.q_seqlen_stride > p.o_seqlen_stride ? p.q_seqlen_stride : p.o_seqlen_stride;
+    if (big * 2 * (p.seqlen_q + 32) + 256 > 0x7fffffffLL) return false;
+    const int64_t nwg = (p.seqlen_q + kBlockM - 1) / kBlockM * p.num_heads_q * p.batch_size;
+    return knobs().zigzag == 2 || nwg <= device_cus();
+}
+inline int64_t zigzag_qtiles(int64_t seqlen_q) { return ((seqlen_q + 127) / 128 + 1) / 2; }
 
 // launch one (dtype, causal, head-dim tile, exact head dim) instantiation on `stream`
 template <class DT, bool C, int kD, bool kExact>

@@ -12,3 +12,8 @@ if [ $# -gt 0 ]; then
   AB_REPS=7 bash scripts/experiments/ab_run.sh "c2 c4 c5" "$@" > $OUT/ab.log 2>&1 || exit 1
   cat $OUT/ab.log
 fi
+# one-rank shares of the 8-way strong split (zigzag layout for the small causal grids)
+for c in c2 c4 c5; do
+  timeout -k 10 200 python bench.py --config $c --world 8 --rank 0 --steps 200 > $OUT/bench_${c}_w8r0.json 2> $OUT/bench_${c}_w8r0.err || exit 1
+  cut -c1-220 $OUT/bench_${c}_w8r0.json
+done

@@ -283,3 +283,68 @@ def test_hip_graph_capture_replay(device, shape):
         eager = m.flash_attn_func(q, k, v, causal=causal)
         assert torch.equal(out, eager)
     assert not torch.equal(out, ref)
+
+
+ZIGZAG = [  # (B, Hq, Hkv, Sq, Sk, D): causal launches that fit one round of the grid
+    (1, 4, 2, 1024, 1024, 128),   # 8 segments -> 4 blocks per head
+    (2, 2, 1, 640, 640, 64),      # 5 segments: the middle one has no partner
+    (1, 2, 2, 700, 900, 128),     # Sq < Sk: bottom-right offset, ragged last segment
+    (1, 2, 1, 600, 333, 128),     # Sq > Sk: rows that see no key
+    (1, 3, 3, 200, 200, 96),      # 2 segments, padded head dim tile
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16], ids=["f16", "bf16"])
+@pytest.mark.parametrize("shape", ZIGZAG, ids=lambda s: "x".join(map(str, s)))
+def test_zigzag_causal_blocks(device, shape, dtype):
+    """Causal launches whose 256-row blocks fit one round of the persistent grid pair the 128-row
+    segments t and nseg - 1 - t (fa_fwd_w4 "Zigzag Q blocks": equal work per block); with the layout
+    forced on and off, both against the oracle, two launches bit-identical."""
+    import flash_attention_cute_amd as m
+    from flash_attention_cute_amd import _debug
+
+    b, hq, hkv, sq, sk, d = shape
+    seed = zlib.crc32(repr((shape, str(dtype), "zz")).encode())
+    q, k, v = make(b, hq, hkv, sq, sk, d, dtype, seed)
+    qd, kd, vd = q.to(device), k.to(device), v.to(device)
+    _debug.set_knobs()
+    try:
+        out = m.flash_attn_func(qd, kd, vd, causal=True)
+        assert _debug.last_path() == "w4" and _debug.last_zigzag()  # the default picks it (small grid)
+        again = m.flash_attn_func(qd, kd, vd, causal=True)
+        _debug.set_zigzag(0)
+        plain = m.flash_attn_func(qd, kd, vd, causal=True)
+        assert not _debug.last_zigzag()
+        torch.cuda.synchronize()
+    finally:
+        _debug.set_zigzag()
+    assert torch.equal(out, again)
+    check(out, q, k, v, d ** -0.5, True, dtype)
+    check(plain, q, k, v, d ** -0.5, True, dtype)
+
+
+def test_zigzag_only_where_it_applies(device):
+    """Non-causal, windowed and large-grid causal launches keep the plain layout; mode 2 forces the
+    zigzag on a large causal grid too (and stays exact), mode 0 keeps it off on a small one."""
+    import flash_attention_cute_amd as m
+    from flash_attention_cute_amd import _debug
+
+    q, k, v = (t.to(device) for t in make(1, 2, 2, 512, 512, 128, torch.float16, 5))
+    try:
+        m.flash_attn_func(q, k, v, causal=False)
+        assert not _debug.last_zigzag()
+        m.flash_attn_window_func(q, k, v, 100, causal=True)
+        assert not _debug.last_zigzag()
+        big = [t.to(device) for t in make(8, 32, 8, 1024, 1024, 128, torch.float16, 6)]  # 1024 blocks
+        ref = m.flash_attn_func(*big, causal=True)
+        assert not _debug.last_zigzag()
+        _debug.set_zigzag(2)
+        zz = m.flash_attn_func(*big, causal=True)
+        assert _debug.last_zigzag()
+        torch.cuda.synchronize()
+        assert (zz.float() - ref.float()).abs().max().item() < 4e-3
+        _debug.set_zigzag(0)
+        m.flash_attn_func(q, k, v, causal=True)
+        assert not _debug.last_zigzag()
+    finally:
+        _debug.set_zigzag()
