@@ -1,5 +1,6 @@
 """Build tagged stamps/experiment variants of the ABI library (only the instantiations that
 scripts/stamps.py c2 / c4 run). usage: python scripts/experiments/build_exp.py tag[:DEF1,DEF2][:flag flag] ..."""
+import os
 import sys
 from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
@@ -16,7 +17,10 @@ def one(spec):
     defs = tuple(x for x in parts[1].split(",") if x) if len(parts) > 1 else ()
     flags = tuple(parts[2].split()) if len(parts) > 2 else ()
     stamps = not tag.startswith("x")  # tags starting with "x": plain experiment builds (no stamps)
-    return _build.build_abi(stamps=stamps, tag=tag, defines=defs, flags=flags, only=ONLY, force=True)
+    # EXP_NOGATE=1: the _asm_check gate's findings become warnings (diagnostic builds such as
+    # FA_EXP_CZERO, which the gate rejects by design)
+    return _build.build_abi(stamps=stamps, tag=tag, defines=defs, flags=flags, only=ONLY, force=True,
+                            gate=os.environ.get("EXP_NOGATE") != "1")
 
 
 with ThreadPoolExecutor(max_workers=4) as ex:

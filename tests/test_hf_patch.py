@@ -518,20 +518,25 @@ def test_patched_llama_static_cache_decode_steps_replay_one_hip_graph(device):
     toks = []
     with torch.no_grad(), warnings.catch_warnings(), patched(ml.LlamaAttention):
         warnings.simplefilter("ignore")
-        out = model(ids, attention_mask=full[:, :n0], position_ids=pid, past_key_values=cache, use_cache=True)
+        out = model(ids, attention_mask=full[:, :n0], position_ids=pid, past_key_values=cache, use_cache=True,
+                    cache_position=torch.arange(n0, device=device))
         toks.append(out.logits[:, -1].argmax(-1, keepdim=True))
         tok_buf, pos_buf = toks[-1].clone(), pid[:, -1:] + 1
+        # the cache slot of the fed token, a device tensor advanced in place: without it the model
+        # derives the slot from the cache's host-side length, which a captured graph bakes in
+        slot_buf = torch.tensor([n0], device=device)
         full[:, n0] = 1
 
         def step():
             return model(tok_buf, attention_mask=full, position_ids=pos_buf, past_key_values=cache,
-                         use_cache=True).logits[:, -1]
+                         use_cache=True, cache_position=slot_buf).logits[:, -1]
 
         def advance(logits, i):  # token i + 1 generated: feed it at the next slot
             toks.append(logits.argmax(-1, keepdim=True))
             tok_buf.copy_(toks[-1])
             full[:, n0 + i] = 1
             pos_buf.add_(1)
+            slot_buf.add_(1)
 
         advance(step(), 1)  # decode step 1 eagerly (it also warms every lazy initialisation up)
         torch.cuda.synchronize()
