@@ -505,6 +505,9 @@ def test_patched_llama_static_cache_decode_steps_replay_one_hip_graph(device):
     assert hf_attention.TRUST_PADDING_MASK is False
     model, ids, mask = tiny_generator(device, True)
     model = model.half()
+    # no EOS: the config's eos id (2) ends row 0 after two tokens in fp16 and generate pads the rest,
+    # while the step loop below keeps generating
+    model.generation_config.eos_token_id = None
     n_new = 24
     with torch.no_grad():
         ref = model.generate(ids, attention_mask=mask, max_new_tokens=n_new, do_sample=False, pad_token_id=0,
