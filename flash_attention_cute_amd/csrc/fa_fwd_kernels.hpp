@@ -1270,11 +1270,10 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // (gap 4ks+2: K_{j+1} pieces, then V_j pieces), and with SM2 the second softmax half of the
     // tile of parity pr (32 units: block u&1, score u>>1 of half 1).
     constexpr int G1 = 4 * KS;
-#ifdef FA_EXP_VEARLY
-    // (experiment) phase 2's first-k-step V^T fragments, read in phase 1's last k-step (its K
-    // fragment buffer is free there) instead of all eight at the phase boundary
+    // phase 2's first-k-step V^T fragments, read in phase 1's last k-step (its K fragment buffer is
+    // free there; V_{j-1}'s ring slot is not a DMA target in this tile) instead of all at the phase
+    // boundary: A/B C2 +0.9 %, C4 +0.5 %, C5 +1.1 %, bit-identical (profiles/r4_ab_batch1.log)
     u32x4 va_pre[DTL];
-#endif
     // AD (A-dead tiles, causal diagonal): bit 0 = block A has no visible score in this tile (its S
     // MFMAs are skipped), bit 1 = nor in the previous tile (its late softmax units are skipped)
     auto phase1 = [&](const char *K, auto PAR, auto SM2, auto DMA, const rsrc_t &kq, const rsrc_t &vq, auto AD)
@@ -1327,7 +1326,6 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #endif
                 }
             }
-#ifdef FA_EXP_VEARLY
             if constexpr (do_sm && ks == KS - 1 && i < DTL) {
                 static_for<2>([&](auto E) {
                     constexpr int n = 2 * i + decltype(E)::value;
@@ -1336,7 +1334,6 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                     va_pre[n >> 1][2 * (n & 1) + 1] = x[1];
                 });
             }
-#endif
             if constexpr (do_dma && i == 2) {
                 if constexpr (ks < NP) dma_q_at<pr * T, ks * 1024>(kq, lds_base, kvo[ks]);
                 else dma_q_at<(2 + c) * T, (ks - NP) * 1024>(vq, lds_base, vvo[ks - NP]);
@@ -1438,13 +1435,10 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             dst[n >> 1][2 * (n & 1)] = x[0];
             dst[n >> 1][2 * (n & 1) + 1] = x[1];
         };
-#ifdef FA_EXP_VEARLY
-        if constexpr (do_sm) {
+        if constexpr (do_sm) {  // (read in phase 1 of the same iteration)
 #pragma unroll
             for (int n = 0; n < DTL; ++n) va[0][n] = va_pre[n];
-        } else
-#endif
-        {
+        } else {
 #pragma unroll
             for (int n = 0; n < 2 * DTL; ++n) rd(0, n, va[0]);
         }
