@@ -126,6 +126,9 @@ def _parse(text: str):
             continue
         if fn is None:
             continue
+        if re.match(r"^\s*\.(section|amdhsa_kernel)\b|^\.Lfunc_end", ln):  # the kernel's code ends (an
+            fn = None                                                     # s_endpgm need not be last)
+            continue
         if ";;#ASMSTART" in ln:
             in_asm = True
             continue
@@ -140,17 +143,18 @@ def _parse(text: str):
         im = _INSN.match(code)
         if not im or im.group(1).startswith("."):
             continue
-        if im.group(1) == "s_endpgm":
-            kernels[fn].append((None, "s_endpgm", [], in_asm, ln))
-            fn = None
-            continue
         ops = [o.strip() for o in (im.group(2) or "").split(",")]
         kernels[fn].append((None, im.group(1), ops, in_asm, ln))
     return kernels
 
 
+_LONGJMP = re.compile(r"\((\.?L\w+)-\.Lpost_getpc\d+\)")
+
+
 def _blocks(insns):
-    """Basic blocks: [(label, [insn]), ...] and successor label lists."""
+    """Basic blocks: [(label, [insn]), ...] and successor label lists. A long branch (hipcc's
+    ``s_getpc_b64`` / ``s_add_u32 s, s, (.LBBn-.Lpost_getpcM)`` / ``s_setpc_b64`` sequence in a
+    kernel too large for 16-bit branch offsets) is an unconditional jump to .LBBn."""
     blocks, cur, lab = [], [], None
     for it in insns:
         if it[0] is not None:  # label
@@ -159,7 +163,7 @@ def _blocks(insns):
             lab, cur = it[0], []
             continue
         cur.append(it)
-        if _BRANCH.match(it[1]) or it[1] == "s_endpgm":
+        if _BRANCH.match(it[1]) or it[1] in ("s_endpgm", "s_setpc_b64"):
             blocks.append((lab, cur))
             lab, cur = None, []
     if cur or lab is not None:
@@ -175,6 +179,19 @@ def _blocks(insns):
                 s.append(index[tgt])
             if last != "s_branch" and i + 1 < len(blocks):
                 s.append(i + 1)
+        elif last == "s_setpc_b64":
+            # the target: the (.LBBn-.Lpost_getpcM) term of the s_add_u32 before it (this block or,
+            # since the .Lpost_getpc label starts a block, the one before)
+            tgt = None
+            for j in (i, i - 1):
+                for it in blocks[j][1] if j >= 0 else []:
+                    m = _LONGJMP.search(it[4])
+                    if m:
+                        tgt = m.group(1)
+            if tgt in index:
+                s.append(index[tgt])
+            else:  # unknown target: every block (conservative)
+                s.extend(range(len(blocks)))
         elif last != "s_endpgm" and i + 1 < len(blocks):
             s.append(i + 1)
         succ.append(s)

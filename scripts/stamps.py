@@ -9,6 +9,7 @@ DMA wait, the barrier; plus the in-kernel clock (s_memtime / s_memrealtime x 100
 usage: python scripts/stamps.py [c2|c3|c4|c5] [w4|p8]   (p8: 8 waves per Q block; p1 = phase A, p2 = B)
 """
 import ctypes
+import os
 import sys
 from pathlib import Path
 
@@ -18,10 +19,14 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 import bench  # noqa: E402
 
-cfg = bench.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "c2"]
+cfg = dict(bench.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "c2"])
+if os.environ.get("STAMPS_SHAPE"):  # "B,Hq,Hkv,S,causal,dtype", e.g. "1,16,4,4096,1,fp16" (C4's 8-way share)
+    b_, hq_, hkv_, s_, c_, dt_ = os.environ["STAMPS_SHAPE"].split(",")
+    cfg.update(B=int(b_), Hq=int(hq_), Hkv=int(hkv_), Sq=int(s_), Sk=int(s_), causal=bool(int(c_)), dtype=dt_,
+               workload=f"shape {os.environ['STAMPS_SHAPE']}")
 variant = sys.argv[2] if len(sys.argv) > 2 else "w4"
 WAVES = 8 if variant == "p8" else 4
-import os  # noqa: E402
+
 
 lib = ctypes.CDLL(os.environ.get("FA_STAMPS_LIB", str(ROOT / "build" / "stamps" / "libfa_gfx950.so")))
 
@@ -51,6 +56,8 @@ buf = torch.zeros(nwg * WAVES * 12, dtype=torch.int64, device=dev)
 stream = torch.cuda.current_stream().cuda_stream
 lib.fa_debug_set_stamps(ctypes.c_void_p(0))
 lib.fa_debug_set_knobs({"w4": 0, "p8": 3}[variant], -1, -1, -1, -1)
+if os.environ.get("STAMPS_ZIGZAG"):  # 0 plain causal blocks, 1 the default rule, 2 always
+    lib.fa_debug_set_zigzag(int(os.environ["STAMPS_ZIGZAG"]))
 import time  # noqa: E402
 
 t0 = time.time()
@@ -102,6 +109,10 @@ for x in range(8):
         print(f"    xcd {x}: blocks {int(sel.sum())}, end {float(e.max() - first) / 100:.1f} us, "
               f"busy {float(xs[:, 9].sum()) / 100:.0f} us, cycles {float(xs[:, 0].sum()) / 1e6:.2f} M, "
               f"clock {float((xs[:, 0] / xs[:, 9]).median()) / 10:.3f} GHz")
+bt = torch.quantile(w0[:, 0], torch.tensor([0.1, 0.5, 0.9, 1.0], dtype=torch.float64))
+btl = torch.quantile(w0[:, 5], torch.tensor([0.1, 0.5, 0.9, 1.0], dtype=torch.float64))
+print(f"  block cycles (wave 0) p10 {bt[0]:.0f}  p50 {bt[1]:.0f}  p90 {bt[2]:.0f}  max {bt[3]:.0f}; "
+      f"tiles p10 {btl[0]:.0f}  p50 {btl[1]:.0f}  p90 {btl[2]:.0f}  max {btl[3]:.0f}")
 for i, nm in [(6, "drain"), (7, "prologue"), (8, "epilogue")]:
     qs = torch.quantile(s[:, i], torch.tensor([0.1, 0.5, 0.9, 0.99], dtype=torch.float64))
     print(f"  {nm:10s} p10 {qs[0]:8.0f}  p50 {qs[1]:8.0f}  p90 {qs[2]:8.0f}  p99 {qs[3]:8.0f}")

@@ -415,6 +415,14 @@ def test_mfma_hazard_rules_on_synthetic_streams():
     loop = ".LBB0_1:\n" + body + "\ts_cbranch_scc1 .LBB0_1\n"
     assert any("R5" in h for h in run(loop.replace(z, "")))  # never zeroed: undefined, then stale
     assert run(loop) == []
+    # code placed after an s_endpgm and reached by a long branch (s_getpc / s_add_u32 (.LBBn - .Lpost_getpc)
+    # / s_setpc_b64, what hipcc emits when a kernel outgrows 16-bit branch offsets) is part of the CFG:
+    # the violation in it is found, and the long branch is not a fall-through into the next block
+    far = (z + "\ts_getpc_b64 s[0:1]\n.Lpost_getpc0:\n\ts_add_u32 s0, s0, (.LBB0_9-.Lpost_getpc0)&4294967295\n"
+           "\ts_addc_u32 s1, s1, (.LBB0_9-.Lpost_getpc0)>>32\n\ts_setpc_b64 s[0:1]\n"
+           ".LBB0_5:\n\tv_accvgpr_read_b32 v50, a0\n\ts_endpgm\n"
+           ".LBB0_9:\n\tv_mov_b32_e32 v4, 0\n" + asm(f"{mf} a[0:15], v[4:7], v[8:11], a[0:15]") + "\ts_nop 15\n\ts_branch .LBB0_5\n")
+    assert [h.split(": ")[1][:2] for h in A.hazards(k + far + ".Lfunc_end0:\n")] == ["R1"]
 
 
 def test_mfma_hazard_gate_passes_the_product_assembly():
