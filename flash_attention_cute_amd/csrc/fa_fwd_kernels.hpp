@@ -834,6 +834,12 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     unsigned long long st_rt0 = __builtin_amdgcn_s_memrealtime();
     uint32_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #define FA_STAMP(v) const uint32_t v = (uint32_t)__builtin_amdgcn_s_memtime()
+#ifdef FA_STAMPS_FINE  // (finer split: phase 2 at the ends of its quarters, phase 1 at its middle)
+    uint32_t st_f[4] = {0, 0, 0, 0}, st_fa[4] = {0, 0, 0, 0};
+#define FA_STAMP_W 16
+#else
+#define FA_STAMP_W 12
+#endif
 #else
     (void)stamps;
 #define FA_STAMP(v)
@@ -1355,6 +1361,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                 });
             }
             FA_SCHED_FENCE();
+#ifdef FA_STAMPS_FINE
+            if constexpr (do_sm && do_dma && g == G1 / 2 - 1) st_f[3] = (uint32_t)__builtin_amdgcn_s_memtime();
+#endif
         });
         if constexpr (do_sm) {
             if constexpr (!pdead) u_fin(pr, 0, Late::hf(kNL - 2), Late::v(kNL - 2));
@@ -1503,6 +1512,10 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                 });
             }
             FA_SCHED_FENCE();
+#ifdef FA_STAMPS_FINE
+            if constexpr (do_sm && (g + 1) % (G2 / 4) == 0 && g + 1 < G2)
+                st_f[(g + 1) / (G2 / 4) - 1] = (uint32_t)__builtin_amdgcn_s_memtime();
+#endif
         });
         if constexpr (do_sm) {
             static_for<NE>([&](auto E) {
@@ -1551,6 +1564,10 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     st_rt0 = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
     for (int i = 0; i < 8; ++i) st_acc[i] = 0;
+#ifdef FA_STAMPS_FINE
+#pragma unroll
+    for (int i = 0; i < 4; ++i) st_fa[i] = 0;
+#endif
 #endif
     kp = kb + (j_lo + 1) * step_k;
     vp = vb + j_lo * step_v;
@@ -1698,6 +1715,12 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             st_acc[2] += sd - sc_;
             st_acc[3] += se - sd;
             st_acc[4] += 1;
+#ifdef FA_STAMPS_FINE
+            st_fa[0] += st_f[0] - sb;
+            st_fa[1] += st_f[1] - st_f[0];
+            st_fa[2] += st_f[2] - st_f[1];
+            st_fa[3] += st_f[3] - sa;
+#endif
         }
 #endif
     };
@@ -1875,7 +1898,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         if (stamps && lane == 0) {
             // per Q block: [total, p1, p2+rescale, dma wait, barrier, tiles, drain (+ next block's
             //  prefetch issue), prologue, epilogue, realtime (100 MHz ticks), start time, xcc]
-            unsigned long long *o = stamps + ((size_t)blk_c * 4 + wave) * 12;
+            unsigned long long *o = stamps + ((size_t)blk_c * 4 + wave) * FA_STAMP_W;
             o[0] = s_end - st_t0;
             for (int i = 0; i < 5; ++i) o[1 + i] = st_acc[i];
             o[6] = s_pipe_end - s_loop_end;
@@ -1884,6 +1907,10 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             o[9] = rt_end - st_rt0;
             o[10] = st_rt0;  // (realtime: one clock for every XCD)
             o[11] = xcc_id();
+#ifdef FA_STAMPS_FINE  // [12..14] phase 2 quarters 1-3 (the 4th: p2+rescale - their sum), [15] phase 1 half 1
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[12 + i] = st_fa[i];
+#endif
         }
     }
 #endif

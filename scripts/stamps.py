@@ -52,7 +52,8 @@ p = P(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), cfg["B"], cfg["Hq"
       *[t.stride(0) for t in st], *[t.stride(1) for t in st], *[t.stride(2) for t in st],
       cfg["D"] ** -0.5 * 1.4426950408889634)
 nwg = cfg["B"] * cfg["Hq"] * ((cfg["Sq"] + 255) // 256)
-buf = torch.zeros(nwg * WAVES * 12, dtype=torch.int64, device=dev)
+W = int(os.environ.get("STAMPS_WIDTH", "12"))  # 16: a -DFA_STAMPS_FINE build (phase sub-splits)
+buf = torch.zeros(nwg * WAVES * W, dtype=torch.int64, device=dev)
 stream = torch.cuda.current_stream().cuda_stream
 lib.fa_debug_set_stamps(ctypes.c_void_p(0))
 lib.fa_debug_set_knobs({"w4": 0, "p8": 3}[variant], -1, -1, -1, -1)
@@ -73,7 +74,7 @@ assert lib.fa_fwd_gfx950(ctypes.byref(p), 0 if dt == torch.float16 else 1, int(c
                          ctypes.c_void_p(stream)) == 0
 torch.cuda.synchronize()
 lib.fa_debug_set_stamps(ctypes.c_void_p(0))
-s = buf.view(-1, 12).cpu().double()
+s = buf.view(-1, W).cpu().double()
 s = s[s[:, 0] > 0]  # records of Q blocks that ran (an empty q-tile block writes none)
 names = ["total", "p1", "p2+resc", "dma_wait", "barrier", "tiles", "drain", "prologue", "epilogue", "realtime"]
 med = s.median(dim=0).values
@@ -83,6 +84,13 @@ for i, nm in enumerate(names):
 tiles = s[:, 5].clamp(min=1)
 for i, nm in [(1, "p1"), (2, "p2+resc"), (3, "dma_wait"), (4, "barrier")]:
     print(f"  per tile {nm:10s} {float((s[:, i] / tiles).median()):8.0f} cycles")
+if W == 16:  # FA_STAMPS_FINE: phase 2 in quarters (8 of its 32 MFMA gaps each), phase 1 in halves
+    q = [float((s[:, i] / tiles).median()) for i in (12, 13, 14)]
+    p2t = float((s[:, 2] / tiles).median())
+    h1 = float((s[:, 15] / tiles).median())
+    p1t = float((s[:, 1] / tiles).median())
+    print(f"  per tile p1 halves          {h1:6.0f} {p1t - h1:6.0f}")
+    print(f"  per tile p2 quarters (+resc) {q[0]:6.0f} {q[1]:6.0f} {q[2]:6.0f} {p2t - sum(q):6.0f}")
 clk = (s[:, 0] / s[:, 9] * 100e6 / 1e9)
 print(f"  in-kernel clock median {float(clk.median()):.3f} GHz")
 
