@@ -91,11 +91,6 @@ struct F16 {
         f16x2 v = __builtin_convertvector((f32x2){lo, hi}, f16x2);
         return __builtin_bit_cast(uint32_t, v);
     }
-    // acc + lo + hi of a packed pair, fp32 accumulate (one v_dot2(c)_f32_f16 against (1, 1))
-    static __device__ __forceinline__ float sum2(uint32_t w, float acc) {
-        return __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, w), __builtin_bit_cast(f16x2, 0x3c003c00u), acc,
-                                      false);
-    }
     // rotate-half RoPE of 8 elements (HF apply_rotary_pos_emb, reference models/rope_attn_fwd.py:8-38):
     // x*cos + rot*sin with rot = -partner (first half) / +partner (second half), fp32, one RNE rounding
     static __device__ __forceinline__ u32x4 rope8(u32x4 v, u32x4 partner, u32x4 c, u32x4 s, bool second) {
@@ -125,12 +120,6 @@ struct BF16 {
     static __device__ __forceinline__ uint32_t pack(float lo, float hi) {
         bf16x2 v = __builtin_convertvector((f32x2){lo, hi}, bf16x2);
         return __builtin_bit_cast(uint32_t, v);
-    }
-    // acc + lo + hi of a packed pair, fp32 accumulate (one v_dot2(c)_f32_bf16 against (1, 1))
-    static __device__ __forceinline__ float sum2(uint32_t w, float acc) {
-        typedef __bf16 bf16x2_ __attribute__((ext_vector_type(2)));
-        return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_, w), __builtin_bit_cast(bf16x2_, 0x3f803f80u),
-                                               acc, false);
     }
     // rotate-half RoPE of 8 elements (HF apply_rotary_pos_emb, reference models/rope_attn_fwd.py:8-38):
     // x*cos + rot*sin with rot = -partner (first half) / +partner (second half), fp32, one RNE rounding
@@ -1239,19 +1228,6 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // P.V operand of its 16-key k-step
     auto u_fin = [&](const int c, const int X, const int hf, const int v) {
         const f32x16 &s = S[c][2 * X + hf];
-#ifdef FA_EXP_DOT2SUM
-        // (experiment) the row sum of the ROUNDED pair, one v_dot2 per pair instead of two adds
-        if (v & 1) {
-            const uint32_t w = DT::pack(s[v - 1], s[v]);
-            float &acc = (16 * hf + v >= kV0) ? st[X].l : st[X].t;
-            acc = DT::sum2(w, (hf == 0 && v == 1) ? 0.f : acc);  // (before any pin of w: the hazard
-            pin(acc);                                           //  recognizer sees the cvt -> dot pair)
-            uint32_t wp = w;
-            pin(wp);
-            P[c][4 * X + 2 * hf + (v >> 3)][(v & 7) >> 1] = wp;
-        }
-        if (true) return;
-#endif
         {
             // the late scores (run after the tile's rescale) add into l, the early ones into t
             // (t restarts every tile: seeded with s[0] + s[1] at v == 1, no copy at v == 0)
