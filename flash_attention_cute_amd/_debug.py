@@ -52,6 +52,8 @@ def lib(debug: bool = False) -> ctypes.CDLL:
         lib.fa_last_error.restype = ctypes.c_char_p
         lib.fa_debug_set_zigzag.argtypes = [ctypes.c_int]
         lib.fa_debug_set_zigzag.restype = None
+        lib.fa_debug_set_split.argtypes = [ctypes.c_int]
+        lib.fa_debug_set_split.restype = None
         lib.fa_debug_last_zigzag.restype = ctypes.c_int
         _libs[debug] = lib
     return _libs[debug]
@@ -93,7 +95,19 @@ def set_zigzag(mode: int | None = None, debug: bool = False) -> None:
 
 def last_zigzag(debug: bool = False) -> bool:
     """Whether the last prefill launch on this thread ran zigzag Q blocks."""
-    return bool(lib(debug).fa_debug_last_zigzag())
+    return lib(debug).fa_debug_last_zigzag() == 1
+
+
+def set_split(mode: int | None = None, debug: bool = False) -> None:
+    """Key-split causal blocks (the op passes the workspace they need): 0 never, 1 when the blocks fit
+    one round of the persistent grid (the default), 2 whenever a workspace is passed; None restores
+    the default."""
+    lib(debug).fa_debug_set_split(-1 if mode is None else int(mode))
+
+
+def last_layout(debug: bool = False) -> str:
+    """Causal block layout of the last prefill launch on this thread: "plain", "zigzag" or "split"."""
+    return {0: "plain", 1: "zigzag", 2: "split"}[lib(debug).fa_debug_last_zigzag()]
 
 
 def forward(q, k, v, softmax_scale=None, causal=False, variant="w8", window_left=-1, w4_grid=None):

@@ -35,7 +35,7 @@ unsigned long long *g_stamps = nullptr;
 thread_local int g_last_path = fa::kPathNone;
 
 fa::Knobs knobs_from_env() {
-    fa::Knobs k{0, 0, 1, fa::kDecTargetWgs, fa::kDecNt, 1};
+    fa::Knobs k{0, 0, 1, fa::kDecTargetWgs, fa::kDecNt, 1, 1};
     if (const char *v = getenv("FA_GFX950_VARIANT"))
         k.variant = !strcmp(v, "w8") ? 1 : !strcmp(v, "w4slow") ? 2 : !strcmp(v, "p8") ? 3 : 0;
     if (const char *e = getenv("FA_W4_GRID")) k.w4_grid = atoll(e) > 0 ? atoll(e) : 0;
@@ -43,6 +43,7 @@ fa::Knobs knobs_from_env() {
     if (const char *e = getenv("FA_DEC_TARGET_WGS")) k.dec_target = atoll(e) > 0 ? atoll(e) : fa::kDecTargetWgs;
     if (const char *e = getenv("FA_DEC_FLAGS")) k.dec_flags = atoi(e);
     if (const char *e = getenv("FA_ZIGZAG")) k.zigzag = atoi(e);
+    if (const char *e = getenv("FA_SPLIT")) k.split = atoi(e);
 #ifdef FA_DEBUG_VARIANTS
     if (k.variant != 0)  // a debug / A-B body replaces the product kernel for the whole process: say so
         fprintf(stderr,
@@ -92,8 +93,15 @@ extern "C" void fa_debug_set_knobs(int variant, int64_t w4_grid, int decode, int
     k.dec_flags = dec_flags < 0 ? d.dec_flags : dec_flags;
 }
 extern "C" int fa_debug_last_path(void) { return g_last_path; }
+// key-split knob (fa_launch.h Knobs::split, env FA_SPLIT): 0 never, 1 when the caller passes a
+// workspace and the causal blocks fit one round (default), 2 whenever a workspace is passed; < 0
+// restores the environment / default value
+extern "C" void fa_debug_set_split(int mode) {
+    knobs_mut().split = mode < 0 ? env_defaults().split : mode;
+}
 // zigzag knob (fa_launch.h Knobs::zigzag): 0 never, 1 when the blocks fit one round, 2 always; < 0
-// restores the environment / default value. Whether the last prefill launch ran zigzag blocks.
+// restores the environment / default value. fa_debug_last_zigzag: the causal block layout of the
+// last prefill launch on this thread: 0 plain, 1 zigzag, 2 key-split.
 extern "C" void fa_debug_set_zigzag(int mode) {
     knobs_mut().zigzag = mode < 0 ? env_defaults().zigzag : mode;
 }
@@ -233,9 +241,19 @@ int dispatch(const fa_fwd_params *params, int dtype, int causal, void *ws, int64
             return causal ? launch_dec<fa::F16, true>(p, a, ws, s) : launch_dec<fa::F16, false>(p, a, ws, s);
         return causal ? launch_dec<fa::BF16, true>(p, a, ws, s) : launch_dec<fa::BF16, false>(p, a, ws, s);
     }
+    fa::PathArgs xa = ranges;
+    if (ws && fa::use_split(p, causal != 0, ranges)) {  // key-split causal blocks (fa_launch.h use_split)
+        if (fa::split_ws_bytes(p) > ws_bytes)
+            return set_err(FA_ERR_INVALID_ARGUMENT, "workspace of %lld bytes is smaller than the %lld required",
+                           (long long)ws_bytes, (long long)fa::split_ws_bytes(p));
+        xa.split_sync = (unsigned *)ws;
+        xa.split_ws = (float *)((char *)ws + fa::split_sync_bytes(p));
+        const hipError_t e = hipMemsetAsync(ws, 0, fa::split_sync_bytes(p), s);
+        if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "hipMemsetAsync failed: %s", hipGetErrorString(e));
+    }
     if (dtype == FA_DTYPE_F16)
-        return causal ? launch<fa::F16, true>(p, s, ranges) : launch<fa::F16, false>(p, s, ranges);
-    return causal ? launch<fa::BF16, true>(p, s, ranges) : launch<fa::BF16, false>(p, s, ranges);
+        return causal ? launch<fa::F16, true>(p, s, xa) : launch<fa::F16, false>(p, s, xa);
+    return causal ? launch<fa::BF16, true>(p, s, xa) : launch<fa::BF16, false>(p, s, xa);
 }
 
 int check_varlen(const fa_varlen_params *v, int dtype, int causal) {
@@ -448,7 +466,7 @@ extern "C" int fa_fwd_gfx950(const fa_fwd_params *params, int dtype, int causal,
 
 extern "C" int64_t fa_fwd_gfx950_workspace_size(const fa_fwd_params *params, int dtype, int causal) {
     if (check_params(params, dtype, causal) != FA_OK) return -1;
-    if (!use_decode(*params)) return 0;
+    if (!use_decode(*params)) return fa::use_split(*params, causal != 0, kNoPath) ? fa::split_ws_bytes(*params) : 0;
     return fa::decode_ws_bytes(*params, fa::decode_plan(*params, fa::kDecMaxSplit));
 }
 

@@ -170,6 +170,13 @@ struct Geo {
 // v_permlane32_swap(vdst=x, src=x): the lower half-wave receives the upper half's x in the src
 // result and keeps its own in vdst; the upper half the other way round. Combining both results
 // therefore gives the (l, l^32) pair reduction with the same value in both lanes.
+// a * fa + b * fb as two rounded products and one rounded sum, never contracted into an fma (the
+// key-split combine: symmetric in its two operands, so bit-identical whichever piece is "a")
+__device__ __forceinline__ float sum_of_products(float a, float fa, float b, float fb) {
+    float x = a * fa, y = b * fb;
+    asm volatile("" : "+v"(x), "+v"(y));
+    return x + y;
+}
 __device__ __forceinline__ float pair_max(float x) {
     auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
     return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
@@ -927,6 +934,14 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // 256 CUs). Block A's rows are always the workgroup's first 128 rows from m0 (the A-dead tiles
     // below follow); block B's rows start rowB rows after block A's (128 for the plain layout).
     const bool zz = kCausal && xa.zigzag;
+    // Key-split causal blocks (xa.split_ws, dense causal launches whose blocks fit one round; the host
+    // passes twice the q-tiles): item 2t + k is piece k of plain q-tile t, over the first (k = 0) or
+    // second (k = 1) half of the block's key tiles. Both pieces of a q-tile are heavy-first
+    // neighbours, so the persistent snake puts a heavy piece and a light one on every workgroup (two
+    // rounds) and no block is longer than half the longest q-tile. Their combine is in the epilogue.
+    const bool spl = kCausal && xa.split_ws != nullptr;
+    auto qtile_of = [&](const Work &wk) { return spl ? wk.qtile >> 1 : wk.qtile; };
+    int split_slot = 0;  // (batch, q-head, plain q-tile) of the current block: its workspace slot
     auto geom_of = [&](const int qtile, const int sq, int &m0o, int &rowbo) __attribute__((always_inline)) {
         if (zz) {
             const int nseg = (sq + 127) >> 7, sB = nseg - 1 - qtile;
@@ -974,7 +989,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         kb = (const char *)p.k_ptr + 2 * (krow0 + (int64_t)hkv * p.k_head_stride);
         vb = (const char *)p.v_ptr + 2 * (vrow0 + (int64_t)hkv * p.v_head_stride);
         ob = (char *)p.o_ptr + 2 * (orow0 + (int64_t)hq * p.o_head_stride);
-        geom_of(wk.qtile, Sq, m0, rowB);
+        geom_of(qtile_of(wk), Sq, m0, rowB);
         // rows interleaved over the waves: block A = rows mw..mw+31 (the workgroup's first half),
         // block B = rows mw+rowB.. (its second half), so the last causal diagonal tiles hold no
         // score of any wave's block A (A-dead tiles, below)
@@ -1002,6 +1017,13 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             const int lo1 = min(m0 + kBlockM, Sq) - 1 + diag - wl;  // the last row's
             j_lo = min(max(lo0, 0) / kBlockN, n_end);
             j_um = min((max(lo1, 0) + kBlockN - 1) / kBlockN, n_end);
+        }
+        if (spl) {  // piece 0: tiles [0, mid); piece 1: [mid, n_end), the diagonal tiles among them
+            const int mid = n_end / 2;
+            if (wk.qtile & 1) j_lo = j_um = mid;
+            else n_end = mid;
+            n_pipe = min(n_pipe, n_end);
+            split_slot = (b * (int)p.num_heads_q + hq) * (n_qtiles >> 1) + (wk.qtile >> 1);
         }
     };
     set_block(decode_work<kCausal>(nwg, xcd + 8 * kblk, n_qtiles, (int)p.num_heads_q, (int)p.head_q_per_group));
@@ -1076,7 +1098,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             row0 = (int64_t)q0 * qs_;
         }
         int m0n;
-        geom_of(wk.qtile, sq, m0n, rb);
+        geom_of(qtile_of(wk), sq, m0n, rb);
         const int mwn = m0n + wave * 32;
         const char *qbn = (const char *)p.q_ptr + 2 * (row0 + (int64_t)wk.hq * p.q_head_stride);
         return make_rsrc_u(qbn + 2 * (int64_t)mwn * qs_, slab_bytes(min(sq - mwn, rb + 32), qs_, D));
@@ -1814,7 +1836,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // Every wave is past this block's last barrier: the Q AGPRs and both K slots are free (the
     // drain reads only a V slot).
     char *const ob_c = ob;
-    const int mw_c = mw, sq_c = Sq, jlo_c = j_lo, rowb_c = rowB;
+    const int mw_c = mw, sq_c = Sq, jlo_c = j_lo, rowb_c = rowB, slot_c = split_slot;
 #ifdef FA_STAMPS
     const uint32_t blk_c = xcd + 8 * kblk;
 #endif
@@ -1855,7 +1877,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     mfma_drain();  // last asm MFMA -> AGPR reads
     const int os_ = (int)p.o_seqlen_stride;
     const rsrc_t orr = make_rsrc(ob_c + 2 * (int64_t)mw_c * os_, slab_bytes(min(sq_c - mw_c, rowb_c + 32), os_, D));
-    auto store_block = [&](const int row, auto OBASE, const float l_tot) {
+    // (key-split blocks: pw = the partner piece's partial O of this block, combined as o * fm + pw * fo)
+    auto store_block = [&](const int row, auto OBASE, const float l_tot, const u32x4 *pw = nullptr, const float fm = 1.f,
+                           const float fo = 0.f) {
         constexpr int ob0 = decltype(OBASE)::value;
         f32x16 o[DTL];
         o[0] = agpr_read16<ob0>();
@@ -1863,6 +1887,19 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         if constexpr (DTL == 4) {
             o[2] = agpr_read16<ob0 + 32>();
             o[3] = agpr_read16<ob0 + 48>();
+        }
+        if (pw) {
+#pragma unroll
+            for (int dt = 0; dt < DTL; ++dt) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const u32x4 x = pw[(dt * 4 + q) * 64 + lane];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)  // (two rounded products, then their sum -- no fma: the
+                                                  // same bits whichever piece arrives second)
+                        o[dt][4 * q + e] = sum_of_products(o[dt][4 * q + e], fm, __uint_as_float(x[e]), fo);
+                }
+            }
         }
         const float inv = (l_tot == 0.f) ? 1.f : 1.f / l_tot;
         const int orow = row * os_ * 2;
@@ -1885,11 +1922,61 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         }
     };
     FA_STAMP(s_masked_end);
-    // row sums: each lane half summed half of the tile's keys
-    const float l0 = pair_sum(st[0].l);
-    const float l1 = pair_sum(st[1].l);
-    store_block(r, IC<0>{}, l0);
-    store_block(r + rowb_c, IC<16 * DTL>{}, l1);
+    if (!spl) {
+        // row sums: each lane half summed half of the tile's keys
+        const float l0 = pair_sum(st[0].l);
+        const float l1 = pair_sum(st[1].l);
+        store_block(r, IC<0>{}, l0);
+        store_block(r + rowb_c, IC<16 * DTL>{}, l1);
+    } else {
+        // ---- key-split block: the two pieces meet per wave. The first to arrive leaves its
+        // unnormalised O (AGPR fragment order, 64 lanes x 16 B per record) and its (nmsc, l, m) per
+        // lane in the workspace and raises the ready flag; the second waits for that flag (the first
+        // has finished its tiles and only stores), rescales both to their larger reference and stores
+        // O. Counters are vector atomics at agent scope (the pieces may run on different XCDs).
+        constexpr int kWaveF = 64 * (32 * DTL + kSplitStatsPerLane);
+        unsigned *sync = xa.split_sync + 2 * ((size_t)slot_c * 4 + wave);
+        u32x4 *wsw = (u32x4 *)(xa.split_ws + ((size_t)slot_c * 4 + wave) * kWaveF);
+        u32x4 *stats = wsw + 8 * DTL * 64;  // after the 2 x DTL x 4 O records
+        uint32_t arrived = 0;
+        if (lane == 0) arrived = __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        arrived = __builtin_amdgcn_readfirstlane(arrived);
+        if (arrived == 0) {
+            static_for<2 * DTL>([&](auto I) {
+                constexpr int i = decltype(I)::value;
+                const f32x16 o = agpr_read16<16 * i>();
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    wsw[(i * 4 + q) * 64 + lane] = (u32x4){__float_as_uint(o[4 * q]), __float_as_uint(o[4 * q + 1]),
+                                                           __float_as_uint(o[4 * q + 2]), __float_as_uint(o[4 * q + 3])};
+            });
+            stats[lane] = (u32x4){__float_as_uint(st[0].nmsc), __float_as_uint(st[1].nmsc), __float_as_uint(st[0].l),
+                                  __float_as_uint(st[1].l)};
+            stats[64 + lane] = (u32x4){__float_as_uint(st[0].m), __float_as_uint(st[1].m), 0u, 0u};
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            if (lane == 0) __hip_atomic_store(sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (lane == 0) {
+                while (__hip_atomic_load(sync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+                    __builtin_amdgcn_s_sleep(8);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            const u32x4 s0 = stats[lane], s1 = stats[64 + lane];
+            float fm[2], fo[2], lt[2];
+#pragma unroll
+            for (int X = 0; X < 2; ++X) {
+                // references: -nmsc (scaled); a row that saw no key in a piece has m = kNeg, O = l = 0
+                const bool sm = st[X].m > 0.5f * kNeg, so = __uint_as_float(s1[X]) > 0.5f * kNeg;
+                const float mm = -st[X].nmsc, mo = -__uint_as_float(s0[X]);
+                const float mt = sm && so ? fmaxf(mm, mo) : (sm ? mm : mo);
+                fm[X] = sm ? __builtin_amdgcn_exp2f(mm - mt) : 0.f;
+                fo[X] = so ? __builtin_amdgcn_exp2f(mo - mt) : 0.f;
+                lt[X] = pair_sum(sum_of_products(st[X].l, fm[X], __uint_as_float(s0[2 + X]), fo[X]));
+            }
+            store_block(r, IC<0>{}, lt[0], wsw, fm[0], fo[0]);
+            store_block(r + rowb_c, IC<16 * DTL>{}, lt[1], wsw + 4 * DTL * 64, fm[1], fo[1]);
+        }
+    }
 #ifdef FA_STAMPS
     {
         __builtin_amdgcn_s_waitcnt(0);
@@ -1938,9 +2025,13 @@ int launch_one(const fa_fwd_params &p, const PathArgs &xa, hipStream_t stream) {
 #else
     constexpr int variant = 0;  // the product library: fa_fwd_w4 only
 #endif
-    PathArgs xz = xa;  // (fa_fwd_w4 / w4slow: zigzag Q blocks for a causal launch that fits one round)
-    xz.zigzag = variant != 1 && use_zigzag(p, C, xa) ? 1 : 0;
-    const int64_t n_qtiles = xz.zigzag ? zigzag_qtiles(p.seqlen_q) : (p.seqlen_q + kBlockM - 1) / kBlockM;
+    // fa_fwd_w4 / w4slow: key-split causal blocks when the dispatcher passed their workspace
+    // (xa.split_ws), else zigzag Q blocks for a causal launch that fits one round
+    PathArgs xz = xa;
+    if (variant == 1) xz.split_ws = nullptr;
+    xz.zigzag = !xz.split_ws && variant != 1 && use_zigzag(p, C, xa) ? 1 : 0;
+    const int64_t n_plain = (p.seqlen_q + kBlockM - 1) / kBlockM;
+    const int64_t n_qtiles = xz.split_ws ? 2 * n_plain : xz.zigzag ? zigzag_qtiles(p.seqlen_q) : n_plain;
     const int64_t nwg = n_qtiles * p.num_heads_q * p.batch_size;
 #ifdef FA_DEBUG_VARIANTS
     if (variant == 1)
@@ -1954,7 +2045,7 @@ int launch_one(const fa_fwd_params &p, const PathArgs &xa, hipStream_t stream) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "HIP launch failed: %s", hipGetErrorString(e));
     set_last_path(variant == 1 ? kPathW8 : variant == 2 ? kPathW4Slow : kPathW4);
-    set_last_zigzag(xz.zigzag);
+    set_last_zigzag(xz.split_ws ? 2 : xz.zigzag);
     return FA_OK;
 }
 

@@ -47,6 +47,7 @@ struct Knobs {
     int64_t dec_target;
     int dec_flags;
     int zigzag;
+    int split;  // key-split causal Q blocks (use_split): 0 never, 1 where they apply (default), 2 always
 };
 
 const Knobs &knobs();
@@ -87,6 +88,11 @@ int64_t device_cus();
 // batch row b (its batch strides apply), or nullptr.
 // zigzag (set by launch_one, never by the dispatchers): causal Q blocks pair the 128-row segments t
 // and nseg - 1 - t (fa_fwd_w4 "Zigzag Q blocks"), for dense causal launches that fit one round.
+// split_ws (set by the dispatcher when the caller passed a workspace, use_split): every causal Q
+// block runs as two pieces over the two halves of its key tiles, on two workgroups; the piece that
+// finishes first leaves its unnormalised O and row statistics in split_ws, the second combines
+// them with its own and stores O (fa_fwd_w4 "Key-split causal blocks"). split_sync: per (block,
+// wave) [arrivals, ready] counters, zeroed by the dispatcher before the launch.
 struct PathArgs {
     const void *cos;
     const void *sin;
@@ -97,6 +103,8 @@ struct PathArgs {
     const int *q_rng, *k_rng;
     const int *k_lo, *k_hi;
     int zigzag;
+    float *split_ws;
+    unsigned *split_sync;
 };
 
 // Whether a prefill launch runs zigzag Q blocks, and its logical q-tile count (blocks per (batch,
@@ -111,6 +119,26 @@ inline bool use_zigzag(const fa_fwd_params &p, bool causal, const PathArgs &xa) 
     return knobs().zigzag == 2 || nwg <= device_cus();
 }
 inline int64_t zigzag_qtiles(int64_t seqlen_q) { return ((seqlen_q + 127) / 128 + 1) / 2; }
+
+// Key-split causal blocks: the same dense causal launches as zigzag whose plain blocks fit one round
+// (knob 1) or always (knob 2). Workspace: the per-(block, wave) sync counters, then per (block,
+// wave) the partial O of its 64 rows (32 * DTL fp32 per lane) and two 16-byte statistic records per lane.
+inline bool use_split(const fa_fwd_params &p, bool causal, const PathArgs &xa) {
+    if (!causal || xa.k_rng || xa.cos || xa.window_left >= 0 || knobs().split == 0 || p.seqlen_q <= 128) return false;
+    const int64_t nwg = (p.seqlen_q + kBlockM - 1) / kBlockM * p.num_heads_q * p.batch_size;
+    return knobs().split == 2 || nwg <= device_cus();
+}
+constexpr int kSplitStatsPerLane = 8;  // floats: (nmsc, l) of blocks A and B, then (m_A, m_B, 0, 0)
+inline int64_t split_wave_floats(int64_t headdim) {
+    return 64 * ((headdim <= 64 ? 2 : 4) * 32 + kSplitStatsPerLane);  // 64 lanes x (2 blocks x DTL x 16 + stats)
+}
+inline int64_t split_blocks(const fa_fwd_params &p) {
+    return (p.seqlen_q + kBlockM - 1) / kBlockM * p.num_heads_q * p.batch_size;
+}
+inline int64_t split_sync_bytes(const fa_fwd_params &p) { return (split_blocks(p) * 4 * 2 * 4 + 255) / 256 * 256; }
+inline int64_t split_ws_bytes(const fa_fwd_params &p) {
+    return split_sync_bytes(p) + split_blocks(p) * 4 * split_wave_floats(p.headdim) * 4;
+}
 
 // launch one (dtype, causal, head-dim tile, exact head dim) instantiation on `stream`
 template <class DT, bool C, int kD, bool kExact>

@@ -104,8 +104,13 @@ int fa_fwd_gfx950(const fa_fwd_params *params, int dtype, int causal, void *stre
  * reference csrc/flash_attention_api.cpp:72-83, or head_q_per_group * Sq <=
  * 64) run a split-KV decode kernel; splitting the keys over more workgroups
  * needs `workspace_bytes` >= fa_fwd_gfx950_workspace_size() of device memory
- * for fp32 partials. With workspace == NULL it behaves exactly like
- * fa_fwd_gfx950 (decode kernel unsplit). The workspace is scratch: it may be
+ * for fp32 partials. A causal prefill whose 256-row blocks fit one round of the
+ * persistent grid (at most one block per CU: a single long sequence, one GPU's
+ * share of a multi-GPU split) splits each block's keys in two pieces on two
+ * workgroups instead; the workspace then holds the first piece's fp32 partial O
+ * and the per-block counters (zeroed by this call on `stream` before the launch).
+ * With workspace == NULL it behaves exactly like fa_fwd_gfx950 (decode kernel
+ * unsplit, causal prefill in zigzag blocks). The workspace is scratch: it may be
  * reused as soon as the launch completes in stream order. 16-byte aligned.
  * No reference counterpart (split-KV is a TODO at reference README.md:20).
  */
@@ -114,7 +119,8 @@ int fa_fwd_gfx950_ws(const fa_fwd_params *params, int dtype, int causal, void *w
 
 /*
  * Bytes of workspace fa_fwd_gfx950_ws wants for these parameters (0 when the
- * launch does not split; -1 when the parameters are invalid). Host-only.
+ * launch does not split; -1 when the parameters are invalid). Host-only (it
+ * queries the current device's CU count for the causal-prefill split).
  */
 int64_t fa_fwd_gfx950_workspace_size(const fa_fwd_params *params, int dtype, int causal);
 
