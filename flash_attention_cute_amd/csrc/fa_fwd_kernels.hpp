@@ -1956,9 +1956,11 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             if (lane == 0) __hip_atomic_store(sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-            if (lane == 0) {
-                while (__hip_atomic_load(sync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+            if (lane == 0) {  // (bounded, ~1 s: a protocol bug ends in a wrong result, never in a hang)
+                for (int it = 0; it < (1 << 22); ++it) {
+                    if (__hip_atomic_load(sync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
                     __builtin_amdgcn_s_sleep(8);
+                }
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             const u32x4 s0 = stats[lane], s1 = stats[64 + lane];
