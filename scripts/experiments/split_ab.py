@@ -17,7 +17,7 @@ shapes = [("c4 share B1 Hq16/4 S4096 f16", 1, 16, 4, 4096, torch.float16),
           ("c5-like B1 Hq32/8 S2048 bf16", 1, 32, 8, 2048, torch.bfloat16),
           ("B1 Hq8/8 S8192 bf16", 1, 8, 8, 8192, torch.bfloat16),
           ("B2 Hq8/2 S4096 f16", 2, 8, 2, 4096, torch.float16)]
-modes = {"split": (None, None), "zigzag": (0, None), "plain": (0, 0)}
+modes = {"split": (1, None), "zigzag": (0, None), "plain": (0, 0)}
 op = torch.ops.flash_attention.forward
 for name, b, hq, hkv, s, dt in shapes:
     q = torch.randn(b, hq, s, 128, device=dev, dtype=dt)

@@ -368,7 +368,7 @@ SPLIT = [  # (B, Hq, Hkv, Sq, Sk, D): causal launches whose 256-row blocks fit o
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16], ids=["f16", "bf16"])
 def test_key_split_causal_blocks(device, shape, dtype):
     """Key-split causal blocks (fa_fwd_w4 "Key-split causal blocks": each block's key tiles in two
-    pieces on two workgroups, the second combining): the op's default for one-round causal grids;
+    pieces on two workgroups, the second combining), knob on, for one-round causal grids;
     against the oracle, two launches bit-identical (the combine does not depend on which piece
     arrives second), any persistent grid size bit-identical, and close to the unsplit layout."""
     import flash_attention_cute_amd as m
@@ -379,6 +379,7 @@ def test_key_split_causal_blocks(device, shape, dtype):
     q, k, v = make(b, hq, hkv, sq, sk, d, dtype, seed)
     qd, kd, vd = q.to(device), k.to(device), v.to(device)
     _debug.set_knobs()
+    _debug.set_split(1)
     try:
         out = m.flash_attn_func(qd, kd, vd, causal=True)
         assert _debug.last_path() == "w4" and _debug.last_layout() == "split"
@@ -390,6 +391,7 @@ def test_key_split_causal_blocks(device, shape, dtype):
         _debug.set_zigzag(0)
         plain = m.flash_attn_func(qd, kd, vd, causal=True)
         assert _debug.last_layout() == "plain"
+        _debug.set_split(1)
         torch.cuda.synchronize()
     finally:
         _debug.set_split()
@@ -410,27 +412,31 @@ def test_key_split_only_with_a_workspace(device):
 
     lib = _debug.lib()
     lib.fa_fwd_gfx950_workspace_size.restype = ctypes.c_int64
-    q, k, v = (t.to(device) for t in make(1, 4, 2, 1024, 1024, 128, torch.float16, 9))
-    o = torch.empty_like(q)
-    p = _debug.FaFwdParams(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), 1, 4, 2, 1024, 1024, 128, 2,
-                           *(t.stride(i) for i in range(3) for t in (q, k, v, o)), 128 ** -0.5 * _debug.LOG2E)
-    need = lib.fa_fwd_gfx950_workspace_size(ctypes.byref(p), 0, 1)
-    assert need > 0 and lib.fa_fwd_gfx950_workspace_size(ctypes.byref(p), 0, 0) == 0
-    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    assert lib.fa_fwd_gfx950(ctypes.byref(p), 0, 1, stream) == 0
-    assert _debug.last_layout() == "zigzag"
-    ws = torch.empty(need, dtype=torch.uint8, device=device)
-    o2 = torch.empty_like(q)
-    p.o_ptr = o2.data_ptr()
-    lib.fa_fwd_gfx950_ws.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
-                                     ctypes.c_void_p]
-    assert lib.fa_fwd_gfx950_ws(ctypes.byref(p), 0, 1, ws.data_ptr(), need - 256, stream) == 1  # too small
-    assert lib.fa_fwd_gfx950_ws(ctypes.byref(p), 0, 1, ws.data_ptr(), need, stream) == 0
-    assert _debug.last_layout() == "split"
-    torch.cuda.synchronize()
-    assert (o.float() - o2.float()).abs().max().item() < 4e-3
-    # 8 x 32 heads x 4 q-tiles = 1024 blocks, four rounds: no workspace (contiguous [B, H, S, D] strides)
-    hs = {"q": 32, "k": 8, "v": 8, "o": 32}
-    strides = [hs[t] * 1024 * 128 for t in "qkvo"] + [1024 * 128] * 4 + [128] * 4
-    pb = _debug.FaFwdParams(0x10000, 0x10000, 0x10000, 0x10000, 8, 32, 8, 1024, 1024, 128, 4, *strides, 0.1)
-    assert lib.fa_fwd_gfx950_workspace_size(ctypes.byref(pb), 0, 1) == 0
+    _debug.set_split(1)
+    try:
+        q, k, v = (t.to(device) for t in make(1, 4, 2, 1024, 1024, 128, torch.float16, 9))
+        o = torch.empty_like(q)
+        p = _debug.FaFwdParams(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), 1, 4, 2, 1024, 1024, 128, 2,
+                               *(t.stride(i) for i in range(3) for t in (q, k, v, o)), 128 ** -0.5 * _debug.LOG2E)
+        need = lib.fa_fwd_gfx950_workspace_size(ctypes.byref(p), 0, 1)
+        assert need > 0 and lib.fa_fwd_gfx950_workspace_size(ctypes.byref(p), 0, 0) == 0
+        stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        assert lib.fa_fwd_gfx950(ctypes.byref(p), 0, 1, stream) == 0
+        assert _debug.last_layout() == "zigzag"
+        ws = torch.empty(need, dtype=torch.uint8, device=device)
+        o2 = torch.empty_like(q)
+        p.o_ptr = o2.data_ptr()
+        lib.fa_fwd_gfx950_ws.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
+                                         ctypes.c_void_p]
+        assert lib.fa_fwd_gfx950_ws(ctypes.byref(p), 0, 1, ws.data_ptr(), need - 256, stream) == 1  # too small
+        assert lib.fa_fwd_gfx950_ws(ctypes.byref(p), 0, 1, ws.data_ptr(), need, stream) == 0
+        assert _debug.last_layout() == "split"
+        torch.cuda.synchronize()
+        assert (o.float() - o2.float()).abs().max().item() < 4e-3
+        # 8 x 32 heads x 4 q-tiles = 1024 blocks, four rounds: no workspace (contiguous [B, H, S, D] strides)
+        hs = {"q": 32, "k": 8, "v": 8, "o": 32}
+        strides = [hs[t] * 1024 * 128 for t in "qkvo"] + [1024 * 128] * 4 + [128] * 4
+        pb = _debug.FaFwdParams(0x10000, 0x10000, 0x10000, 0x10000, 8, 32, 8, 1024, 1024, 128, 4, *strides, 0.1)
+        assert lib.fa_fwd_gfx950_workspace_size(ctypes.byref(pb), 0, 1) == 0
+    finally:
+        _debug.set_split()
