@@ -47,7 +47,7 @@ struct Knobs {
     int64_t dec_target;
     int dec_flags;
     int zigzag;
-    int split;  // key-split causal Q blocks (use_split): 0 never, 1 where they apply (default), 2 always
+    int split;  // key-split causal Q blocks (use_split): 0 never (default), 1 where they apply, 2 always
 };
 
 const Knobs &knobs();
