@@ -177,6 +177,25 @@ __device__ __forceinline__ float sum_of_products(float a, float fa, float b, flo
     asm volatile("" : "+v"(x), "+v"(y));
     return x + y;
 }
+// device-scope (sc1) vector memory accesses of the key-split workspace: written through to the level
+// every XCD reads and read from there, so neither side needs an agent-scope fence (a release /
+// acquire fence writes back / invalidates the whole L2 of the XCD, K/V lines of every other
+// workgroup included). The caller waits vmcnt before using a load or publishing after stores.
+__device__ __forceinline__ void st_dev(u32x4 *p, const u32x4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ u32x4 ld_dev(const u32x4 *p) {
+    u32x4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// device-scope (sc1) atomic add returning the old value: performed where every XCD sees it
+__device__ __forceinline__ unsigned atomic_add_dev(unsigned *p, unsigned v) {
+    unsigned old;
+    asm volatile("global_atomic_add %0, %1, %2, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(old) : "v"(p), "v"(v) : "memory");
+    return old;
+}
 __device__ __forceinline__ float pair_max(float x) {
     auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
     return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
@@ -1877,9 +1896,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     mfma_drain();  // last asm MFMA -> AGPR reads
     const int os_ = (int)p.o_seqlen_stride;
     const rsrc_t orr = make_rsrc(ob_c + 2 * (int64_t)mw_c * os_, slab_bytes(min(sq_c - mw_c, rowb_c + 32), os_, D));
-    // (key-split blocks: pw = the partner piece's partial O of this block, combined as o * fm + pw * fo)
-    auto store_block = [&](const int row, auto OBASE, const float l_tot, const u32x4 *pw = nullptr, const float fm = 1.f,
-                           const float fo = 0.f) {
+    auto store_block = [&](const int row, auto OBASE, const float l_tot) {
         constexpr int ob0 = decltype(OBASE)::value;
         f32x16 o[DTL];
         o[0] = agpr_read16<ob0>();
@@ -1887,19 +1904,6 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         if constexpr (DTL == 4) {
             o[2] = agpr_read16<ob0 + 32>();
             o[3] = agpr_read16<ob0 + 48>();
-        }
-        if (pw) {
-#pragma unroll
-            for (int dt = 0; dt < DTL; ++dt) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const u32x4 x = pw[(dt * 4 + q) * 64 + lane];
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)  // (two rounded products, then their sum -- no fma: the
-                                                  // same bits whichever piece arrives second)
-                        o[dt][4 * q + e] = sum_of_products(o[dt][4 * q + e], fm, __uint_as_float(x[e]), fo);
-                }
-            }
         }
         const float inv = (l_tot == 0.f) ? 1.f : 1.f / l_tot;
         const int orow = row * os_ * 2;
@@ -1921,6 +1925,40 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             }
         }
     };
+    // key-split blocks: the same stores of o * fm + pw * fo (pw: the partner piece's partial O of this
+    // block), one d-tile at a time to keep the live registers of the epilogue low. Two rounded
+    // products and their rounded sum -- no fma: the same bits whichever piece arrives second.
+    auto store_block_combined = [&](const int row, auto OBASE, const float l_tot, const u32x4 *pw, const float fm,
+                                    const float fo) {
+        constexpr int ob0 = decltype(OBASE)::value;
+        const float inv = (l_tot == 0.f) ? 1.f : 1.f / l_tot;
+        const int orow = row * os_ * 2;
+        static_for<DTL>([&](auto DD) {
+            constexpr int dt = decltype(DD)::value;
+            f32x16 od = agpr_read16<ob0 + 16 * dt>();
+            u32x4 xs[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) xs[q] = ld_dev(pw + (dt * 4 + q) * 64 + lane);
+            wait_vm();
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) od[4 * q + e] = sum_of_products(od[4 * q + e], fm, __uint_as_float(xs[q][e]), fo);
+            }
+#pragma unroll
+            for (int gp = 0; gp < 4; gp += 2) {
+                const uint32_t a0 = DT::pack(od[4 * gp + 0] * inv, od[4 * gp + 1] * inv);
+                const uint32_t a1 = DT::pack(od[4 * gp + 2] * inv, od[4 * gp + 3] * inv);
+                const uint32_t b0 = DT::pack(od[4 * gp + 4] * inv, od[4 * gp + 5] * inv);
+                const uint32_t b1 = DT::pack(od[4 * gp + 6] * inv, od[4 * gp + 7] * inv);
+                const auto x0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+                const auto x1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+                const int d0 = dt * 32 + 8 * (gp + h);
+                __builtin_amdgcn_raw_buffer_store_b128((u32x4){x0[0], x1[0], x0[1], x1[1]}, orr,
+                                                       (kExactD || d0 < D) ? orow + 2 * d0 : 0x7ffffff0, 0, 0);
+            }
+        });
+    };
     FA_STAMP(s_masked_end);
     if (!spl) {
         // row sums: each lane half summed half of the tile's keys
@@ -1939,7 +1977,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         u32x4 *wsw = (u32x4 *)(xa.split_ws + ((size_t)slot_c * 4 + wave) * kWaveF);
         u32x4 *stats = wsw + 8 * DTL * 64;  // after the 2 x DTL x 4 O records
         uint32_t arrived = 0;
-        if (lane == 0) arrived = __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) arrived = atomic_add_dev(sync, 1u);
         arrived = __builtin_amdgcn_readfirstlane(arrived);
         if (arrived == 0) {
             static_for<2 * DTL>([&](auto I) {
@@ -1947,13 +1985,14 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                 const f32x16 o = agpr_read16<16 * i>();
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
-                    wsw[(i * 4 + q) * 64 + lane] = (u32x4){__float_as_uint(o[4 * q]), __float_as_uint(o[4 * q + 1]),
-                                                           __float_as_uint(o[4 * q + 2]), __float_as_uint(o[4 * q + 3])};
+                    st_dev(wsw + (i * 4 + q) * 64 + lane,
+                           (u32x4){__float_as_uint(o[4 * q]), __float_as_uint(o[4 * q + 1]), __float_as_uint(o[4 * q + 2]),
+                                   __float_as_uint(o[4 * q + 3])});
             });
-            stats[lane] = (u32x4){__float_as_uint(st[0].nmsc), __float_as_uint(st[1].nmsc), __float_as_uint(st[0].l),
-                                  __float_as_uint(st[1].l)};
-            stats[64 + lane] = (u32x4){__float_as_uint(st[0].m), __float_as_uint(st[1].m), 0u, 0u};
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            st_dev(stats + lane, (u32x4){__float_as_uint(st[0].nmsc), __float_as_uint(st[1].nmsc),
+                                         __float_as_uint(st[0].l), __float_as_uint(st[1].l)});
+            st_dev(stats + 64 + lane, (u32x4){__float_as_uint(st[0].m), __float_as_uint(st[1].m), 0u, 0u});
+            wait_vm();  // (every lane's records written through before the flag)
             if (lane == 0) __hip_atomic_store(sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             if (lane == 0) {  // (bounded, ~1 s: a protocol bug ends in a wrong result, never in a hang)
@@ -1962,8 +2001,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                     __builtin_amdgcn_s_sleep(8);
                 }
             }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            const u32x4 s0 = stats[lane], s1 = stats[64 + lane];
+            const u32x4 s0 = ld_dev(stats + lane), s1 = ld_dev(stats + 64 + lane);
+            wait_vm();
             float fm[2], fo[2], lt[2];
 #pragma unroll
             for (int X = 0; X < 2; ++X) {
@@ -1975,8 +2014,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                 fo[X] = so ? __builtin_amdgcn_exp2f(mo - mt) : 0.f;
                 lt[X] = pair_sum(sum_of_products(st[X].l, fm[X], __uint_as_float(s0[2 + X]), fo[X]));
             }
-            store_block(r, IC<0>{}, lt[0], wsw, fm[0], fo[0]);
-            store_block(r + rowb_c, IC<16 * DTL>{}, lt[1], wsw + 4 * DTL * 64, fm[1], fo[1]);
+            store_block_combined(r, IC<0>{}, lt[0], wsw, fm[0], fo[0]);
+            store_block_combined(r + rowb_c, IC<16 * DTL>{}, lt[1], wsw + 4 * DTL * 64, fm[1], fo[1]);
         }
     }
 #ifdef FA_STAMPS
