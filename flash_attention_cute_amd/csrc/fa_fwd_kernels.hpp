@@ -177,24 +177,35 @@ __device__ __forceinline__ float sum_of_products(float a, float fa, float b, flo
     asm volatile("" : "+v"(x), "+v"(y));
     return x + y;
 }
-// device-scope (sc1) vector memory accesses of the key-split workspace: written through to the level
-// every XCD reads and read from there, so neither side needs an agent-scope fence (a release /
-// acquire fence writes back / invalidates the whole L2 of the XCD, K/V lines of every other
-// workgroup included). The caller waits vmcnt before using a load or publishing after stores.
-__device__ __forceinline__ void st_dev(u32x4 *p, const u32x4 v) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+// Key-split workspace accesses (the pieces of a block are paired on one XCD by fa_fwd_w4's work
+// order, for speed; correctness does not rest on it): every record store is a 16-B write-through
+// (sc1) store drained by its wave before the flag, the flag an agent-scope (sc1) store, the
+// counter an agent-scope atomic, and every load of a record or statistic an sc1 load (bypasses
+// this CU's L1) behind the poll. That is the placement-independent hand-off with no agent-scope
+// fence (a release / acquire fence writes back / invalidates the whole L2 of the XCD, the K/V lines
+// of every other workgroup included: measured, the layout ran at half speed with them). Inline asm
+// (the builtin forms cost the D=128 causal kernels a spilled VGPR), so: the loads and their wait in
+// ONE statement with early-clobber outputs (hipcc counts no asm load), and every 16-B store ends in
+// s_nop 1 (hipcc may otherwise overwrite its data registers before the store has read them).
+__device__ __forceinline__ void st_ws(u32x4 *p, const u32x4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
-__device__ __forceinline__ u32x4 ld_dev(const u32x4 *p) {
-    u32x4 v;
-    asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
-    return v;
+// four records 64 x 16 B apart (p, p + 64, p + 128, p + 192), landed
+__device__ __forceinline__ void ld_ws4(const u32x4 *p, u32x4 (&x)[4]) {
+    asm volatile("global_load_dwordx4 %0, %4, off sc1\n\tglobal_load_dwordx4 %1, %4, off offset:1024 sc1\n\t"
+                 "global_load_dwordx4 %2, %4, off offset:2048 sc1\n\tglobal_load_dwordx4 %3, %4, off offset:3072 sc1\n\t"
+                 "s_waitcnt vmcnt(0)"
+                 : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3])
+                 : "v"(p)
+                 : "memory");
 }
-__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// device-scope (sc1) atomic add returning the old value: performed where every XCD sees it
-__device__ __forceinline__ unsigned atomic_add_dev(unsigned *p, unsigned v) {
-    unsigned old;
-    asm volatile("global_atomic_add %0, %1, %2, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(old) : "v"(p), "v"(v) : "memory");
-    return old;
+// two records (p, p + 64), landed
+__device__ __forceinline__ void ld_ws2(const u32x4 *p, u32x4 &x0, u32x4 &x1) {
+    asm volatile("global_load_dwordx4 %0, %2, off sc1\n\tglobal_load_dwordx4 %1, %2, off offset:1024 sc1\n\t"
+                 "s_waitcnt vmcnt(0)"
+                 : "=&v"(x0), "=&v"(x1)
+                 : "v"(p)
+                 : "memory");
 }
 __device__ __forceinline__ float pair_max(float x) {
     auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
@@ -941,7 +952,25 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     const uint32_t nwg = (uint32_t)n_qtiles * (uint32_t)p.num_heads_q * (uint32_t)p.batch_size;
     const uint32_t xcd = blockIdx.x & 7, cx = blockIdx.x >> 3;
     const uint32_t gx = (gridDim.x - xcd + 7) >> 3;  // workgroups of this XCD
-    const uint32_t cnt = (nwg - xcd + 7) >> 3;       // Q blocks of this XCD
+    // key-split blocks (below): the XCD-aware order runs over (batch, q-head, q-tile) units, each
+    // expanded into its two pieces next to each other in ONE XCD's list -- the pieces meet through
+    // that XCD's L2
+    const bool spl = kCausal && xa.split_ws != nullptr;
+    const uint32_t nunits = spl ? nwg >> 1 : nwg;
+    const uint32_t cnt = spl ? 2 * ((nunits - xcd + 7) >> 3) : (nwg - xcd + 7) >> 3;  // Q blocks of this XCD
+    auto work_of = [&](const uint32_t k) __attribute__((always_inline)) {
+        if (!spl)
+            return decode_work<kCausal>(nwg, xcd + 8 * k, n_qtiles, (int)p.num_heads_q, (int)p.head_q_per_group);
+        Work w = decode_work<kCausal>(nunits, xcd + 8 * (k >> 1), n_qtiles >> 1, (int)p.num_heads_q,
+                                      (int)p.head_q_per_group);
+        w.qtile = 2 * w.qtile + (int)(k & 1);  // (item 2t + piece)
+        // (wave-uniform: said so, or the block's buffer descriptors may land in VGPRs, which the
+        // LDS-DMA asm cannot take)
+        w.qtile = __builtin_amdgcn_readfirstlane(w.qtile);
+        w.hq = __builtin_amdgcn_readfirstlane(w.hq);
+        w.b = __builtin_amdgcn_readfirstlane(w.b);
+        return w;
+    };
     auto block_of = [&](const uint32_t rnd) { return rnd * gx + ((rnd & 1) ? gx - 1 - cx : cx); };
     uint32_t rnd = 0, kblk = block_of(0);
     if (kblk >= cnt) return;
@@ -956,9 +985,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // Key-split causal blocks (xa.split_ws, dense causal launches whose blocks fit one round; the host
     // passes twice the q-tiles): item 2t + k is piece k of plain q-tile t, over the first (k = 0) or
     // second (k = 1) half of the block's key tiles. Both pieces of a q-tile are heavy-first
-    // neighbours, so the persistent snake puts a heavy piece and a light one on every workgroup (two
-    // rounds) and no block is longer than half the longest q-tile. Their combine is in the epilogue.
-    const bool spl = kCausal && xa.split_ws != nullptr;
+    // neighbours of one XCD's list, so the persistent snake puts a heavy piece and a light one on
+    // every workgroup (two rounds) and no block is longer than half the longest q-tile. Their
+    // combine is in the epilogue.
     auto qtile_of = [&](const Work &wk) { return spl ? wk.qtile >> 1 : wk.qtile; };
     int split_slot = 0;  // (batch, q-head, plain q-tile) of the current block: its workspace slot
     auto geom_of = [&](const int qtile, const int sq, int &m0o, int &rowbo) __attribute__((always_inline)) {
@@ -1045,7 +1074,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             split_slot = (b * (int)p.num_heads_q + hq) * (n_qtiles >> 1) + (wk.qtile >> 1);
         }
     };
-    set_block(decode_work<kCausal>(nwg, xcd + 8 * kblk, n_qtiles, (int)p.num_heads_q, (int)p.head_q_per_group));
+    set_block(work_of(kblk));
 
     // ---- Q: this wave's 64 rows, B-operand fragments straight from HBM into AGPRs ----------
     // lane (h, r) of block X holds Q[mw + rowB*X + r][16*ks + 8*h + 0..7]; rows >= Sq read as 0.
@@ -1132,7 +1161,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         qn = 0;
         qnt = 0;
         if (kn < cnt) {
-            wk_next = decode_work<kCausal>(nwg, xcd + 8 * kn, n_qtiles, (int)p.num_heads_q, (int)p.head_q_per_group);
+            wk_next = work_of(kn);
             if (kQL && !rope_q) {
                 qnr = q_rsrc_of(wk_next, rowB_next);
                 qnt = NQP;
@@ -1142,7 +1171,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     if (!rope_q) {
         if constexpr (kQL != 0) {
             int rb0;
-            const rsrc_t qr0 = q_rsrc_of(decode_work<kCausal>(nwg, xcd + 8 * kblk, n_qtiles, (int)p.num_heads_q, (int)p.head_q_per_group), rb0);
+            const rsrc_t qr0 = q_rsrc_of(work_of(kblk), rb0);
             static_for<NQP>([&](auto N) { q_piece(qr0, decltype(N)::value, rb0); });
         } else {
             load_q();
@@ -1937,9 +1966,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             constexpr int dt = decltype(DD)::value;
             f32x16 od = agpr_read16<ob0 + 16 * dt>();
             u32x4 xs[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) xs[q] = ld_dev(pw + (dt * 4 + q) * 64 + lane);
-            wait_vm();
+            ld_ws4(pw + dt * 4 * 64 + lane, xs);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
 #pragma unroll
@@ -1971,13 +1998,13 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         // unnormalised O (AGPR fragment order, 64 lanes x 16 B per record) and its (nmsc, l, m) per
         // lane in the workspace and raises the ready flag; the second waits for that flag (the first
         // has finished its tiles and only stores), rescales both to their larger reference and stores
-        // O. Counters are vector atomics at agent scope (the pieces may run on different XCDs).
+        // O. (The pieces run on one XCD by work_of's order; the accesses do not rely on it.)
         constexpr int kWaveF = 64 * (32 * DTL + kSplitStatsPerLane);
         unsigned *sync = xa.split_sync + 2 * ((size_t)slot_c * 4 + wave);
         u32x4 *wsw = (u32x4 *)(xa.split_ws + ((size_t)slot_c * 4 + wave) * kWaveF);
         u32x4 *stats = wsw + 8 * DTL * 64;  // after the 2 x DTL x 4 O records
         uint32_t arrived = 0;
-        if (lane == 0) arrived = atomic_add_dev(sync, 1u);
+        if (lane == 0) arrived = __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         arrived = __builtin_amdgcn_readfirstlane(arrived);
         if (arrived == 0) {
             static_for<2 * DTL>([&](auto I) {
@@ -1985,14 +2012,14 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                 const f32x16 o = agpr_read16<16 * i>();
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
-                    st_dev(wsw + (i * 4 + q) * 64 + lane,
-                           (u32x4){__float_as_uint(o[4 * q]), __float_as_uint(o[4 * q + 1]), __float_as_uint(o[4 * q + 2]),
-                                   __float_as_uint(o[4 * q + 3])});
+                    st_ws(wsw + (i * 4 + q) * 64 + lane,
+                          (u32x4){__float_as_uint(o[4 * q]), __float_as_uint(o[4 * q + 1]), __float_as_uint(o[4 * q + 2]),
+                                  __float_as_uint(o[4 * q + 3])});
             });
-            st_dev(stats + lane, (u32x4){__float_as_uint(st[0].nmsc), __float_as_uint(st[1].nmsc),
-                                         __float_as_uint(st[0].l), __float_as_uint(st[1].l)});
-            st_dev(stats + 64 + lane, (u32x4){__float_as_uint(st[0].m), __float_as_uint(st[1].m), 0u, 0u});
-            wait_vm();  // (every lane's records written through before the flag)
+            st_ws(stats + lane, (u32x4){__float_as_uint(st[0].nmsc), __float_as_uint(st[1].nmsc),
+                                        __float_as_uint(st[0].l), __float_as_uint(st[1].l)});
+            st_ws(stats + 64 + lane, (u32x4){__float_as_uint(st[0].m), __float_as_uint(st[1].m), 0u, 0u});
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (every lane's records written through before the flag)
             if (lane == 0) __hip_atomic_store(sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             if (lane == 0) {  // (bounded, ~1 s: a protocol bug ends in a wrong result, never in a hang)
@@ -2001,8 +2028,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                     __builtin_amdgcn_s_sleep(8);
                 }
             }
-            const u32x4 s0 = ld_dev(stats + lane), s1 = ld_dev(stats + 64 + lane);
-            wait_vm();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: loads stay below the poll)
+            u32x4 s0, s1;
+            ld_ws2(stats + lane, s0, s1);
             float fm[2], fo[2], lt[2];
 #pragma unroll
             for (int X = 0; X < 2; ++X) {

@@ -17,6 +17,10 @@ shapes = [("c4 share B1 Hq16/4 S4096 f16", 1, 16, 4, 4096, torch.float16),
           ("c5-like B1 Hq32/8 S2048 bf16", 1, 32, 8, 2048, torch.bfloat16),
           ("B1 Hq8/8 S8192 bf16", 1, 8, 8, 8192, torch.bfloat16),
           ("B2 Hq8/2 S4096 f16", 2, 8, 2, 4096, torch.float16)]
+if "--sweep" in sys.argv:  # where the layout pays: sequence length x one-round grid fill (256 CUs)
+    shapes = [(f"B1 Hq{h}/{max(h // 4, 1)} S{s} bf16 ({h * ((s + 255) // 256)} blocks)", 1, h, max(h // 4, 1), s, torch.bfloat16)
+              for s in (1024, 2048, 3072, 4096, 6144, 8192) for h in (4, 8, 16, 32, 64)
+              if 64 <= h * ((s + 255) // 256) <= 256]
 modes = {"split": (1, None), "zigzag": (0, None), "plain": (0, 0)}
 op = torch.ops.flash_attention.forward
 for name, b, hq, hkv, s, dt in shapes:
