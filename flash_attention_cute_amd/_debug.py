@@ -99,9 +99,9 @@ def last_zigzag(debug: bool = False) -> bool:
 
 
 def set_split(mode: int | None = None, debug: bool = False) -> None:
-    """Key-split causal blocks (the op passes the workspace they need): 0 never, 1 when the blocks fit
-    one round of the persistent grid (the default), 2 whenever a workspace is passed; None restores
-    the default."""
+    """Key-split causal blocks (the op passes the workspace they need): 0 never, 1 where measured
+    faster than zigzag (the default: one-round grids with long enough keys, fa_launch.h use_split),
+    2 whenever a workspace is passed; None restores the default."""
     lib(debug).fa_debug_set_split(-1 if mode is None else int(mode))
 
 

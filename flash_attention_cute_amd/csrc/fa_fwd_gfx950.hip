@@ -35,7 +35,7 @@ unsigned long long *g_stamps = nullptr;
 thread_local int g_last_path = fa::kPathNone;
 
 fa::Knobs knobs_from_env() {
-    fa::Knobs k{0, 0, 1, fa::kDecTargetWgs, fa::kDecNt, 1, 0};
+    fa::Knobs k{0, 0, 1, fa::kDecTargetWgs, fa::kDecNt, 1, 1};
     if (const char *v = getenv("FA_GFX950_VARIANT"))
         k.variant = !strcmp(v, "w8") ? 1 : !strcmp(v, "w4slow") ? 2 : !strcmp(v, "p8") ? 3 : 0;
     if (const char *e = getenv("FA_W4_GRID")) k.w4_grid = atoll(e) > 0 ? atoll(e) : 0;
@@ -93,8 +93,8 @@ extern "C" void fa_debug_set_knobs(int variant, int64_t w4_grid, int decode, int
     k.dec_flags = dec_flags < 0 ? d.dec_flags : dec_flags;
 }
 extern "C" int fa_debug_last_path(void) { return g_last_path; }
-// key-split knob (fa_launch.h Knobs::split, env FA_SPLIT): 0 never (default), 1 when the caller passes
-// a workspace and the causal blocks fit one round, 2 whenever a workspace is passed; < 0
+// key-split knob (fa_launch.h Knobs::split, env FA_SPLIT): 0 never, 1 (default) when the caller passes
+// a workspace and use_split's measured rule holds, 2 whenever a workspace is passed; < 0
 // restores the environment / default value
 extern "C" void fa_debug_set_split(int mode) {
     knobs_mut().split = mode < 0 ? env_defaults().split : mode;

@@ -47,7 +47,7 @@ struct Knobs {
     int64_t dec_target;
     int dec_flags;
     int zigzag;
-    int split;  // key-split causal Q blocks (use_split): 0 never (default), 1 where they apply, 2 always
+    int split;  // key-split causal Q blocks (use_split): 0 never, 1 where measured faster (default), 2 always
 };
 
 const Knobs &knobs();
@@ -120,13 +120,18 @@ inline bool use_zigzag(const fa_fwd_params &p, bool causal, const PathArgs &xa) 
 }
 inline int64_t zigzag_qtiles(int64_t seqlen_q) { return ((seqlen_q + 127) / 128 + 1) / 2; }
 
-// Key-split causal blocks: the same dense causal launches as zigzag whose plain blocks fit one round
-// (knob 1) or always (knob 2). Workspace: the per-(block, wave) sync counters, then per (block,
+// Key-split causal blocks: dense causal launches (no varlen, window or RoPE) when the caller passes
+// the workspace. Knob 1 (default): where measured faster than zigzag (profiles/r4_split_sweep.log,
+// same-process A/B): the plain blocks fit one round of the grid and the keys are long enough for
+// each half to carry the piece's extra block start and combine -- at least 3072 keys, or 2048 when
+// the plain blocks fill at most half the CUs (+12 to +44 %; a full round at 1024-2048 keys lost
+// 9-26 %). Knob 2: always (tests). Workspace: the per-(block, wave) sync counters, then per (block,
 // wave) the partial O of its 64 rows (32 * DTL fp32 per lane) and two 16-byte statistic records per lane.
 inline bool use_split(const fa_fwd_params &p, bool causal, const PathArgs &xa) {
     if (!causal || xa.k_rng || xa.cos || xa.window_left >= 0 || knobs().split == 0 || p.seqlen_q <= 128) return false;
-    const int64_t nwg = (p.seqlen_q + kBlockM - 1) / kBlockM * p.num_heads_q * p.batch_size;
-    return knobs().split == 2 || nwg <= device_cus();
+    if (knobs().split == 2) return true;
+    const int64_t nwg = (p.seqlen_q + kBlockM - 1) / kBlockM * p.num_heads_q * p.batch_size, cus = device_cus();
+    return nwg <= cus && (p.seqlen_kv >= 3072 || (p.seqlen_kv >= 2048 && 2 * nwg <= cus));
 }
 constexpr int kSplitStatsPerLane = 8;  // floats: (nmsc, l) of blocks A and B, then (m_A, m_B, 0, 0)
 inline int64_t split_wave_floats(int64_t headdim) {

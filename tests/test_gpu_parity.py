@@ -368,7 +368,8 @@ SPLIT = [  # (B, Hq, Hkv, Sq, Sk, D): causal launches whose 256-row blocks fit o
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16], ids=["f16", "bf16"])
 def test_key_split_causal_blocks(device, shape, dtype):
     """Key-split causal blocks (fa_fwd_w4 "Key-split causal blocks": each block's key tiles in two
-    pieces on two workgroups, the second combining), knob on, for one-round causal grids;
+    pieces on two workgroups, the second combining), knob 2 (always; the default rule picks long
+    one-round grids);
     against the oracle, two launches bit-identical (the combine does not depend on which piece
     arrives second), any persistent grid size bit-identical, and close to the unsplit layout."""
     import flash_attention_cute_amd as m
@@ -379,7 +380,7 @@ def test_key_split_causal_blocks(device, shape, dtype):
     q, k, v = make(b, hq, hkv, sq, sk, d, dtype, seed)
     qd, kd, vd = q.to(device), k.to(device), v.to(device)
     _debug.set_knobs()
-    _debug.set_split(1)
+    _debug.set_split(2)
     try:
         out = m.flash_attn_func(qd, kd, vd, causal=True)
         assert _debug.last_path() == "w4" and _debug.last_layout() == "split"
@@ -391,7 +392,6 @@ def test_key_split_causal_blocks(device, shape, dtype):
         _debug.set_zigzag(0)
         plain = m.flash_attn_func(qd, kd, vd, causal=True)
         assert _debug.last_layout() == "plain"
-        _debug.set_split(1)
         torch.cuda.synchronize()
     finally:
         _debug.set_split()
@@ -405,14 +405,15 @@ def test_key_split_causal_blocks(device, shape, dtype):
 def test_key_split_only_with_a_workspace(device):
     """The C-ABI runs key-split blocks only when the caller passes the workspace
     fa_fwd_gfx950_workspace_size asks for (the torch op does); without one (plain fa_fwd_gfx950) the
-    same launch runs zigzag blocks; non-causal and large causal grids ask for none."""
+    same launch runs zigzag blocks; non-causal launches ask for none, nor (default knob) large causal
+    grids or short keys."""
     import ctypes
 
     from flash_attention_cute_amd import _debug
 
     lib = _debug.lib()
     lib.fa_fwd_gfx950_workspace_size.restype = ctypes.c_int64
-    _debug.set_split(1)
+    _debug.set_split(2)
     try:
         q, k, v = (t.to(device) for t in make(1, 4, 2, 1024, 1024, 128, torch.float16, 9))
         o = torch.empty_like(q)
@@ -433,10 +434,17 @@ def test_key_split_only_with_a_workspace(device):
         assert _debug.last_layout() == "split"
         torch.cuda.synchronize()
         assert (o.float() - o2.float()).abs().max().item() < 4e-3
-        # 8 x 32 heads x 4 q-tiles = 1024 blocks, four rounds: no workspace (contiguous [B, H, S, D] strides)
-        hs = {"q": 32, "k": 8, "v": 8, "o": 32}
-        strides = [hs[t] * 1024 * 128 for t in "qkvo"] + [1024 * 128] * 4 + [128] * 4
-        pb = _debug.FaFwdParams(0x10000, 0x10000, 0x10000, 0x10000, 8, 32, 8, 1024, 1024, 128, 4, *strides, 0.1)
-        assert lib.fa_fwd_gfx950_workspace_size(ctypes.byref(pb), 0, 1) == 0
+        # default knob: 8 x 32 heads x 4 q-tiles = 1024 blocks, four rounds, and this one-round 1024-key
+        # launch ask for none; 8 heads x 16 q-tiles of 4096 keys (128 blocks) does (contiguous strides)
+        _debug.set_split()
+        assert lib.fa_fwd_gfx950_workspace_size(ctypes.byref(p), 0, 1) == 0
+
+        def params(b, hq, hkv, s):
+            hs = {"q": hq, "k": hkv, "v": hkv, "o": hq}
+            strides = [hs[t] * s * 128 for t in "qkvo"] + [s * 128] * 4 + [128] * 4
+            return _debug.FaFwdParams(0x10000, 0x10000, 0x10000, 0x10000, b, hq, hkv, s, s, 128, 4, *strides, 0.1)
+
+        assert lib.fa_fwd_gfx950_workspace_size(ctypes.byref(params(8, 32, 8, 1024)), 0, 1) == 0
+        assert lib.fa_fwd_gfx950_workspace_size(ctypes.byref(params(1, 8, 2, 4096)), 0, 1) > 0
     finally:
         _debug.set_split()
