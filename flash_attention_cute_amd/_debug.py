@@ -54,8 +54,6 @@ def lib(debug: bool = False) -> ctypes.CDLL:
         lib.fa_debug_set_zigzag.restype = None
         lib.fa_debug_set_split.argtypes = [ctypes.c_int]
         lib.fa_debug_set_split.restype = None
-        lib.fa_debug_set_split_pieces.argtypes = [ctypes.c_int]
-        lib.fa_debug_set_split_pieces.restype = None
         lib.fa_debug_last_zigzag.restype = ctypes.c_int
         _libs[debug] = lib
     return _libs[debug]
@@ -105,11 +103,6 @@ def set_split(mode: int | None = None, debug: bool = False) -> None:
     faster than zigzag (the default: one-round grids with long enough keys, fa_launch.h use_split),
     2 whenever a workspace is passed; None restores the default."""
     lib(debug).fa_debug_set_split(-1 if mode is None else int(mode))
-
-
-def set_split_pieces(pieces: int | None = None, debug: bool = False) -> None:
-    """Pieces per key-split block: 0 the dispatcher's rule, 2 or 4 forced; None restores the default."""
-    lib(debug).fa_debug_set_split_pieces(-1 if pieces is None else int(pieces))
 
 
 def last_layout(debug: bool = False) -> str:

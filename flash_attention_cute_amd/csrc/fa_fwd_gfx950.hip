@@ -35,7 +35,7 @@ unsigned long long *g_stamps = nullptr;
 thread_local int g_last_path = fa::kPathNone;
 
 fa::Knobs knobs_from_env() {
-    fa::Knobs k{0, 0, 1, fa::kDecTargetWgs, fa::kDecNt, 1, 1, 0};
+    fa::Knobs k{0, 0, 1, fa::kDecTargetWgs, fa::kDecNt, 1, 1};
     if (const char *v = getenv("FA_GFX950_VARIANT"))
         k.variant = !strcmp(v, "w8") ? 1 : !strcmp(v, "w4slow") ? 2 : !strcmp(v, "p8") ? 3 : 0;
     if (const char *e = getenv("FA_W4_GRID")) k.w4_grid = atoll(e) > 0 ? atoll(e) : 0;
@@ -44,7 +44,6 @@ fa::Knobs knobs_from_env() {
     if (const char *e = getenv("FA_DEC_FLAGS")) k.dec_flags = atoi(e);
     if (const char *e = getenv("FA_ZIGZAG")) k.zigzag = atoi(e);
     if (const char *e = getenv("FA_SPLIT")) k.split = atoi(e);
-    if (const char *e = getenv("FA_SPLIT_P")) k.split_p = atoi(e);
 #ifdef FA_DEBUG_VARIANTS
     if (k.variant != 0)  // a debug / A-B body replaces the product kernel for the whole process: say so
         fprintf(stderr,
@@ -99,11 +98,6 @@ extern "C" int fa_debug_last_path(void) { return g_last_path; }
 // restores the environment / default value
 extern "C" void fa_debug_set_split(int mode) {
     knobs_mut().split = mode < 0 ? env_defaults().split : mode;
-}
-// pieces per key-split block (Knobs::split_p, env FA_SPLIT_P): 0 the rule, 2 or 4 forced; < 0
-// restores the environment / default value
-extern "C" void fa_debug_set_split_pieces(int pieces) {
-    knobs_mut().split_p = pieces < 0 ? env_defaults().split_p : pieces;
 }
 // zigzag knob (fa_launch.h Knobs::zigzag): 0 never, 1 when the blocks fit one round, 2 always; < 0
 // restores the environment / default value. fa_debug_last_zigzag: the causal block layout of the
@@ -248,12 +242,10 @@ int dispatch(const fa_fwd_params *params, int dtype, int causal, void *ws, int64
         return causal ? launch_dec<fa::BF16, true>(p, a, ws, s) : launch_dec<fa::BF16, false>(p, a, ws, s);
     }
     fa::PathArgs xa = ranges;
-    const int np = ws ? fa::split_pieces(p, causal != 0, ranges) : 0;
-    if (np) {  // key-split causal blocks (fa_launch.h split_pieces)
-        if (fa::split_ws_bytes(p, np) > ws_bytes)
+    if (ws && fa::use_split(p, causal != 0, ranges)) {  // key-split causal blocks (fa_launch.h use_split)
+        if (fa::split_ws_bytes(p) > ws_bytes)
             return set_err(FA_ERR_INVALID_ARGUMENT, "workspace of %lld bytes is smaller than the %lld required",
-                           (long long)ws_bytes, (long long)fa::split_ws_bytes(p, np));
-        xa.split_lg = np == 4 ? 2 : 1;
+                           (long long)ws_bytes, (long long)fa::split_ws_bytes(p));
         xa.split_sync = (unsigned *)ws;
         xa.split_ws = (float *)((char *)ws + fa::split_sync_bytes(p));
         const hipError_t e = hipMemsetAsync(ws, 0, fa::split_sync_bytes(p), s);
@@ -474,10 +466,7 @@ extern "C" int fa_fwd_gfx950(const fa_fwd_params *params, int dtype, int causal,
 
 extern "C" int64_t fa_fwd_gfx950_workspace_size(const fa_fwd_params *params, int dtype, int causal) {
     if (check_params(params, dtype, causal) != FA_OK) return -1;
-    if (!use_decode(*params)) {
-        const int np = fa::split_pieces(*params, causal != 0, kNoPath);
-        return np ? fa::split_ws_bytes(*params, np) : 0;
-    }
+    if (!use_decode(*params)) return fa::use_split(*params, causal != 0, kNoPath) ? fa::split_ws_bytes(*params) : 0;
     return fa::decode_ws_bytes(*params, fa::decode_plan(*params, fa::kDecMaxSplit));
 }
 

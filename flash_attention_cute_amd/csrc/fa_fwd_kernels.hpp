@@ -170,12 +170,12 @@ struct Geo {
 // v_permlane32_swap(vdst=x, src=x): the lower half-wave receives the upper half's x in the src
 // result and keeps its own in vdst; the upper half the other way round. Combining both results
 // therefore gives the (l, l^32) pair reduction with the same value in both lanes.
-// a * f rounded, never contracted into an fma with a following add (the key-split combine sums
-// rounded products in piece order: the same bits whichever piece combines)
-__device__ __forceinline__ float rounded_product(float a, float f) {
-    float x = a * f;
-    asm volatile("" : "+v"(x));
-    return x;
+// a * fa + b * fb as two rounded products and one rounded sum, never contracted into an fma (the
+// key-split combine: symmetric in its two operands, so bit-identical whichever piece is "a")
+__device__ __forceinline__ float sum_of_products(float a, float fa, float b, float fb) {
+    float x = a * fa, y = b * fb;
+    asm volatile("" : "+v"(x), "+v"(y));
+    return x + y;
 }
 // Key-split workspace accesses (the pieces of a block are paired on one XCD by fa_fwd_w4's work
 // order, for speed; correctness does not rest on it): every record store is a 16-B write-through
@@ -953,19 +953,17 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     const uint32_t xcd = blockIdx.x & 7, cx = blockIdx.x >> 3;
     const uint32_t gx = (gridDim.x - xcd + 7) >> 3;  // workgroups of this XCD
     // key-split blocks (below): the XCD-aware order runs over (batch, q-head, q-tile) units, each
-    // expanded into its P = 2^slg pieces next to each other in ONE XCD's list -- the pieces meet
-    // through that XCD's L2
+    // expanded into its two pieces next to each other in ONE XCD's list -- the pieces meet through
+    // that XCD's L2
     const bool spl = kCausal && xa.split_ws != nullptr;
-    const int slg = spl ? xa.split_lg : 0;
-    const uint32_t npc = 1u << slg;  // pieces per block
-    const uint32_t nunits = nwg >> slg;
-    const uint32_t cnt = ((nunits - xcd + 7) >> 3) << slg;  // Q blocks (pieces) of this XCD
+    const uint32_t nunits = spl ? nwg >> 1 : nwg;
+    const uint32_t cnt = spl ? 2 * ((nunits - xcd + 7) >> 3) : (nwg - xcd + 7) >> 3;  // Q blocks of this XCD
     auto work_of = [&](const uint32_t k) __attribute__((always_inline)) {
         if (!spl)
             return decode_work<kCausal>(nwg, xcd + 8 * k, n_qtiles, (int)p.num_heads_q, (int)p.head_q_per_group);
-        Work w = decode_work<kCausal>(nunits, xcd + 8 * (k >> slg), n_qtiles >> slg, (int)p.num_heads_q,
+        Work w = decode_work<kCausal>(nunits, xcd + 8 * (k >> 1), n_qtiles >> 1, (int)p.num_heads_q,
                                       (int)p.head_q_per_group);
-        w.qtile = (w.qtile << slg) + (int)(k & (npc - 1));  // (item P t + piece)
+        w.qtile = 2 * w.qtile + (int)(k & 1);  // (item 2t + piece)
         // (wave-uniform: said so, or the block's buffer descriptors may land in VGPRs, which the
         // LDS-DMA asm cannot take)
         w.qtile = __builtin_amdgcn_readfirstlane(w.qtile);
@@ -985,13 +983,13 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // below follow); block B's rows start rowB rows after block A's (128 for the plain layout).
     const bool zz = kCausal && xa.zigzag;
     // Key-split causal blocks (xa.split_ws, dense causal launches whose blocks fit one round; the host
-    // passes P = 2^split_lg times the q-tiles): item P t + k is piece k of plain q-tile t, over the
-    // k-th of P equal runs of the block's key tiles. The pieces of a q-tile are heavy-first
+    // passes twice the q-tiles): item 2t + k is piece k of plain q-tile t, over the first (k = 0) or
+    // second (k = 1) half of the block's key tiles. Both pieces of a q-tile are heavy-first
     // neighbours of one XCD's list, so the persistent snake puts a heavy piece and a light one on
-    // every workgroup and no block is longer than 1/P of the longest q-tile. Their combine is in the
-    // epilogue.
-    auto qtile_of = [&](const Work &wk) { return wk.qtile >> slg; };
-    int split_slot = 0;  // 4 x (batch, q-head, plain q-tile) of the current block + its piece
+    // every workgroup (two rounds) and no block is longer than half the longest q-tile. Their
+    // combine is in the epilogue.
+    auto qtile_of = [&](const Work &wk) { return spl ? wk.qtile >> 1 : wk.qtile; };
+    int split_slot = 0;  // (batch, q-head, plain q-tile) of the current block: its workspace slot
     auto geom_of = [&](const int qtile, const int sq, int &m0o, int &rowbo) __attribute__((always_inline)) {
         if (zz) {
             const int nseg = (sq + 127) >> 7, sB = nseg - 1 - qtile;
@@ -1068,12 +1066,12 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             j_lo = min(max(lo0, 0) / kBlockN, n_end);
             j_um = min((max(lo1, 0) + kBlockN - 1) / kBlockN, n_end);
         }
-        if (spl) {  // piece k: tiles [k n_end / P, (k + 1) n_end / P), the diagonal ones in the last
-            const int piece = wk.qtile & (int)(npc - 1);
-            if (piece) j_lo = j_um = (piece * n_end) >> slg;
-            n_end = ((piece + 1) * n_end) >> slg;
+        if (spl) {  // piece 0: tiles [0, mid); piece 1: [mid, n_end), the diagonal tiles among them
+            const int mid = n_end / 2;
+            if (wk.qtile & 1) j_lo = j_um = mid;
+            else n_end = mid;
             n_pipe = min(n_pipe, n_end);
-            split_slot = (((b * (int)p.num_heads_q + hq) * (n_qtiles >> slg) + (wk.qtile >> slg)) << 2) + piece;
+            split_slot = (b * (int)p.num_heads_q + hq) * (n_qtiles >> 1) + (wk.qtile >> 1);
         }
     };
     set_block(work_of(kblk));
@@ -1886,7 +1884,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // Every wave is past this block's last barrier: the Q AGPRs and both K slots are free (the
     // drain reads only a V slot).
     char *const ob_c = ob;
-    const int mw_c = mw, sq_c = Sq, jlo_c = j_lo, rowb_c = rowB, slot_c = split_slot >> 2, piece_c = split_slot & 3;
+    const int mw_c = mw, sq_c = Sq, jlo_c = j_lo, rowb_c = rowB, slot_c = split_slot;
 #ifdef FA_STAMPS
     const uint32_t blk_c = xcd + 8 * kblk;
 #endif
@@ -1956,34 +1954,24 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             }
         }
     };
-    // key-split blocks: the same stores of sum_k o_k * f_k over the P pieces in index order (the
-    // own piece's o from the AGPRs, the others' from their workspace records ws[k] + rec), one
-    // d-tile at a time to keep the live registers of the epilogue low. Rounded products, rounded
-    // sums, no fma: the same bits whichever piece arrives last.
-    auto store_block_combined = [&](const int row, auto OBASE, const float l_tot, auto ws, const int rec,
-                                    const float *f) {
+    // key-split blocks: the same stores of o * fm + pw * fo (pw: the partner piece's partial O of this
+    // block), one d-tile at a time to keep the live registers of the epilogue low. Two rounded
+    // products and their rounded sum -- no fma: the same bits whichever piece arrives second.
+    auto store_block_combined = [&](const int row, auto OBASE, const float l_tot, const u32x4 *pw, const float fm,
+                                    const float fo) {
         constexpr int ob0 = decltype(OBASE)::value;
         const float inv = (l_tot == 0.f) ? 1.f : 1.f / l_tot;
         const int orow = row * os_ * 2;
         static_for<DTL>([&](auto DD) {
             constexpr int dt = decltype(DD)::value;
-            f32x16 od;
-            static_for<4>([&](auto K) {
-                constexpr int k = decltype(K)::value;
-                if (k < (int)npc) {
-                    f32x16 x;
-                    if (k == piece_c) {
-                        x = agpr_read16<ob0 + 16 * dt>();
-                    } else {
-                        u32x4 xs[4];
-                        ld_ws4(ws(k) + rec + dt * 4 * 64 + lane, xs);
+            f32x16 od = agpr_read16<ob0 + 16 * dt>();
+            u32x4 xs[4];
+            ld_ws4(pw + dt * 4 * 64 + lane, xs);
 #pragma unroll
-                        for (int e = 0; e < 16; ++e) x[e] = __uint_as_float(xs[e >> 2][e & 3]);
-                    }
+            for (int q = 0; q < 4; ++q) {
 #pragma unroll
-                    for (int e = 0; e < 16; ++e) od[e] = k == 0 ? rounded_product(x[e], f[k]) : od[e] + rounded_product(x[e], f[k]);
-                }
-            });
+                for (int e = 0; e < 4; ++e) od[4 * q + e] = sum_of_products(od[4 * q + e], fm, __uint_as_float(xs[q][e]), fo);
+            }
 #pragma unroll
             for (int gp = 0; gp < 4; gp += 2) {
                 const uint32_t a0 = DT::pack(od[4 * gp + 0] * inv, od[4 * gp + 1] * inv);
@@ -2006,24 +1994,19 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         store_block(r, IC<0>{}, l0);
         store_block(r + rowb_c, IC<16 * DTL>{}, l1);
     } else {
-        // ---- key-split block: the P pieces meet per wave. Each of the first P - 1 to arrive leaves
-        // its unnormalised O (AGPR fragment order, 64 lanes x 16 B per record) and its (nmsc, l, m)
-        // per lane in its own workspace slot and counts itself written; the last waits for all P - 1
-        // (they have finished their tiles and only store), rescales every piece to the largest
-        // reference and stores O. (The pieces run on one XCD by work_of's order; the accesses do not
-        // rely on it.)
+        // ---- key-split block: the two pieces meet per wave. The first to arrive leaves its
+        // unnormalised O (AGPR fragment order, 64 lanes x 16 B per record) and its (nmsc, l, m) per
+        // lane in the workspace and raises the ready flag; the second waits for that flag (the first
+        // has finished its tiles and only stores), rescales both to their larger reference and stores
+        // O. (The pieces run on one XCD by work_of's order; the accesses do not rely on it.)
         constexpr int kWaveF = 64 * (32 * DTL + kSplitStatsPerLane);
-        constexpr int kStats = 8 * DTL * 64;  // (records: the 2 x DTL x 4 O records, then 2 statistics)
         unsigned *sync = xa.split_sync + 2 * ((size_t)slot_c * 4 + wave);
-        // piece k's records: slot ((block, wave), k)
-        auto ws = [&](const int k) {
-            return (u32x4 *)(xa.split_ws + (((((size_t)slot_c * 4 + wave) << slg) + k) * kWaveF));
-        };
+        u32x4 *wsw = (u32x4 *)(xa.split_ws + ((size_t)slot_c * 4 + wave) * kWaveF);
+        u32x4 *stats = wsw + 8 * DTL * 64;  // after the 2 x DTL x 4 O records
         uint32_t arrived = 0;
         if (lane == 0) arrived = __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         arrived = __builtin_amdgcn_readfirstlane(arrived);
-        if (arrived + 1 < npc) {
-            u32x4 *const wsw = ws(piece_c);
+        if (arrived == 0) {
             static_for<2 * DTL>([&](auto I) {
                 constexpr int i = decltype(I)::value;
                 const f32x16 o = agpr_read16<16 * i>();
@@ -2033,62 +2016,34 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                           (u32x4){__float_as_uint(o[4 * q]), __float_as_uint(o[4 * q + 1]), __float_as_uint(o[4 * q + 2]),
                                   __float_as_uint(o[4 * q + 3])});
             });
-            st_ws(wsw + kStats + lane, (u32x4){__float_as_uint(st[0].nmsc), __float_as_uint(st[1].nmsc),
-                                                __float_as_uint(st[0].l), __float_as_uint(st[1].l)});
-            st_ws(wsw + kStats + 64 + lane, (u32x4){__float_as_uint(st[0].m), __float_as_uint(st[1].m), 0u, 0u});
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (every lane's records written through before the count)
-            if (lane == 0) __hip_atomic_fetch_add(sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            st_ws(stats + lane, (u32x4){__float_as_uint(st[0].nmsc), __float_as_uint(st[1].nmsc),
+                                        __float_as_uint(st[0].l), __float_as_uint(st[1].l)});
+            st_ws(stats + 64 + lane, (u32x4){__float_as_uint(st[0].m), __float_as_uint(st[1].m), 0u, 0u});
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (every lane's records written through before the flag)
+            if (lane == 0) __hip_atomic_store(sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             if (lane == 0) {  // (bounded, ~1 s: a protocol bug ends in a wrong result, never in a hang)
                 for (int it = 0; it < (1 << 22); ++it) {
-                    if (__hip_atomic_load(sync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 >= npc) break;
+                    if (__hip_atomic_load(sync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
                     __builtin_amdgcn_s_sleep(8);
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: loads stay below the poll)
-            // piece k's reference -nmsc, row sum and max (x = 0 / 1 / 2), the own piece's from
-            // registers; a row that saw no key in a piece has m = kNeg, O = l = 0 (weight 0)
-            auto stat = [&](const int k, const int X, float &ref, float &l, bool &has) __attribute__((always_inline)) {
-                if (k == piece_c) {
-                    ref = -st[X].nmsc;
-                    l = st[X].l;
-                    has = st[X].m > 0.5f * kNeg;
-                } else {
-                    u32x4 s0, s1;
-                    ld_ws2(ws(k) + kStats + lane, s0, s1);
-                    ref = -__uint_as_float(s0[X]);
-                    l = __uint_as_float(s0[2 + X]);
-                    has = __uint_as_float(s1[X]) > 0.5f * kNeg;
-                }
-            };
-            float f[2][4], lt[2];
+            u32x4 s0, s1;
+            ld_ws2(stats + lane, s0, s1);
+            float fm[2], fo[2], lt[2];
 #pragma unroll
             for (int X = 0; X < 2; ++X) {
-                float mt = kNeg;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    if (k < (int)npc) {
-                        float ref, l;
-                        bool has;
-                        stat(k, X, ref, l, has);
-                        if (has) mt = fmaxf(mt, ref);
-                    }
-                }
-                float l = 0.f;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    if (k < (int)npc) {
-                        float ref, lk;
-                        bool has;
-                        stat(k, X, ref, lk, has);
-                        f[X][k] = has ? __builtin_amdgcn_exp2f(ref - mt) : 0.f;
-                        l = k == 0 ? rounded_product(lk, f[X][k]) : l + rounded_product(lk, f[X][k]);
-                    }
-                }
-                lt[X] = pair_sum(l);
+                // references: -nmsc (scaled); a row that saw no key in a piece has m = kNeg, O = l = 0
+                const bool sm = st[X].m > 0.5f * kNeg, so = __uint_as_float(s1[X]) > 0.5f * kNeg;
+                const float mm = -st[X].nmsc, mo = -__uint_as_float(s0[X]);
+                const float mt = sm && so ? fmaxf(mm, mo) : (sm ? mm : mo);
+                fm[X] = sm ? __builtin_amdgcn_exp2f(mm - mt) : 0.f;
+                fo[X] = so ? __builtin_amdgcn_exp2f(mo - mt) : 0.f;
+                lt[X] = pair_sum(sum_of_products(st[X].l, fm[X], __uint_as_float(s0[2 + X]), fo[X]));
             }
-            store_block_combined(r, IC<0>{}, lt[0], ws, 0, f[0]);
-            store_block_combined(r + rowb_c, IC<16 * DTL>{}, lt[1], ws, 4 * DTL * 64, f[1]);
+            store_block_combined(r, IC<0>{}, lt[0], wsw, fm[0], fo[0]);
+            store_block_combined(r + rowb_c, IC<16 * DTL>{}, lt[1], wsw + 4 * DTL * 64, fm[1], fo[1]);
         }
     }
 #ifdef FA_STAMPS
@@ -2145,7 +2100,7 @@ int launch_one(const fa_fwd_params &p, const PathArgs &xa, hipStream_t stream) {
     if (variant == 1) xz.split_ws = nullptr;
     xz.zigzag = !xz.split_ws && variant != 1 && use_zigzag(p, C, xa) ? 1 : 0;
     const int64_t n_plain = (p.seqlen_q + kBlockM - 1) / kBlockM;
-    const int64_t n_qtiles = xz.split_ws ? n_plain << xz.split_lg : xz.zigzag ? zigzag_qtiles(p.seqlen_q) : n_plain;
+    const int64_t n_qtiles = xz.split_ws ? 2 * n_plain : xz.zigzag ? zigzag_qtiles(p.seqlen_q) : n_plain;
     const int64_t nwg = n_qtiles * p.num_heads_q * p.batch_size;
 #ifdef FA_DEBUG_VARIANTS
     if (variant == 1)

@@ -47,8 +47,7 @@ struct Knobs {
     int64_t dec_target;
     int dec_flags;
     int zigzag;
-    int split;    // key-split causal Q blocks (split_pieces): 0 never, 1 where measured faster (default), 2 always
-    int split_p;  // pieces per key-split block: 0 by split_pieces' rule (default), 2 or 4 forced (FA_SPLIT_P)
+    int split;  // key-split causal Q blocks (use_split): 0 never, 1 where measured faster (default), 2 always
 };
 
 const Knobs &knobs();
@@ -89,11 +88,11 @@ int64_t device_cus();
 // batch row b (its batch strides apply), or nullptr.
 // zigzag (set by launch_one, never by the dispatchers): causal Q blocks pair the 128-row segments t
 // and nseg - 1 - t (fa_fwd_w4 "Zigzag Q blocks"), for dense causal launches that fit one round.
-// split_ws (set by the dispatcher when the caller passed a workspace, split_pieces): every causal Q
-// block runs as P = 2^split_lg pieces over P runs of its key tiles, on P workgroups; each piece but
-// the last to finish leaves its unnormalised O and row statistics in split_ws, the last combines
+// split_ws (set by the dispatcher when the caller passed a workspace, use_split): every causal Q
+// block runs as two pieces over the two halves of its key tiles, on two workgroups; the piece that
+// finishes first leaves its unnormalised O and row statistics in split_ws, the second combines
 // them with its own and stores O (fa_fwd_w4 "Key-split causal blocks"). split_sync: per (block,
-// wave) [arrivals, written] counters, zeroed by the dispatcher before the launch.
+// wave) [arrivals, ready] counters, zeroed by the dispatcher before the launch.
 struct PathArgs {
     const void *cos;
     const void *sin;
@@ -106,7 +105,6 @@ struct PathArgs {
     int zigzag;
     float *split_ws;
     unsigned *split_sync;
-    int split_lg;
 };
 
 // Whether a prefill launch runs zigzag Q blocks, and its logical q-tile count (blocks per (batch,
@@ -129,14 +127,12 @@ inline int64_t zigzag_qtiles(int64_t seqlen_q) { return ((seqlen_q + 127) / 128 
 // the plain blocks fill at most half the CUs (+12 to +44 %; a full round at 1024-2048 keys lost
 // 9-26 %). Knob 2: always (tests). Workspace: the per-(block, wave) sync counters, then per (block,
 // wave) the partial O of its 64 rows (32 * DTL fp32 per lane) and two 16-byte statistic records per lane.
-inline int split_pieces(const fa_fwd_params &p, bool causal, const PathArgs &xa) {
-    if (!causal || xa.k_rng || xa.cos || xa.window_left >= 0 || knobs().split == 0 || p.seqlen_q <= 128) return 0;
+inline bool use_split(const fa_fwd_params &p, bool causal, const PathArgs &xa) {
+    if (!causal || xa.k_rng || xa.cos || xa.window_left >= 0 || knobs().split == 0 || p.seqlen_q <= 128) return false;
+    if (knobs().split == 2) return true;
     const int64_t nwg = (p.seqlen_q + kBlockM - 1) / kBlockM * p.num_heads_q * p.batch_size, cus = device_cus();
-    const int np = knobs().split_p == 2 || knobs().split_p == 4 ? knobs().split_p : 2;
-    if (knobs().split == 2) return np;
-    return nwg <= cus && (p.seqlen_kv >= 3072 || (p.seqlen_kv >= 2048 && 2 * nwg <= cus)) ? np : 0;
+    return nwg <= cus && (p.seqlen_kv >= 3072 || (p.seqlen_kv >= 2048 && 2 * nwg <= cus));
 }
-inline bool use_split(const fa_fwd_params &p, bool causal, const PathArgs &xa) { return split_pieces(p, causal, xa) != 0; }
 constexpr int kSplitStatsPerLane = 8;  // floats: (nmsc, l) of blocks A and B, then (m_A, m_B, 0, 0)
 inline int64_t split_wave_floats(int64_t headdim) {
     return 64 * ((headdim <= 64 ? 2 : 4) * 32 + kSplitStatsPerLane);  // 64 lanes x (2 blocks x DTL x 16 + stats)
@@ -145,8 +141,8 @@ inline int64_t split_blocks(const fa_fwd_params &p) {
     return (p.seqlen_q + kBlockM - 1) / kBlockM * p.num_heads_q * p.batch_size;
 }
 inline int64_t split_sync_bytes(const fa_fwd_params &p) { return (split_blocks(p) * 4 * 2 * 4 + 255) / 256 * 256; }
-inline int64_t split_ws_bytes(const fa_fwd_params &p, int pieces) {
-    return split_sync_bytes(p) + split_blocks(p) * 4 * pieces * split_wave_floats(p.headdim) * 4;
+inline int64_t split_ws_bytes(const fa_fwd_params &p) {
+    return split_sync_bytes(p) + split_blocks(p) * 4 * split_wave_floats(p.headdim) * 4;
 }
 
 // launch one (dtype, causal, head-dim tile, exact head dim) instantiation on `stream`

@@ -15,7 +15,11 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 import bench  # noqa: E402
 
-cfg = bench.CONFIGS[sys.argv[1]]
+cfg = dict(bench.CONFIGS[sys.argv[1]])
+if os.environ.get("AB_SHAPE"):  # B,Hq,Hkv,S,D,dtype,causal: a shape of its own (e.g. one rank's share)
+    b_, hq_, hkv_, s_, d_, dt_, c_ = os.environ["AB_SHAPE"].split(",")
+    cfg.update(B=int(b_), Hq=int(hq_), Hkv=int(hkv_), Sq=int(s_), Sk=int(s_), D=int(d_), dtype=dt_, causal=c_ == "1")
+    cfg.pop("W", None)
 VARIANTS = {"w4": 0, "w8": 1, "w4slow": 2, "p8": 3}
 specs = [a.split("@") for a in sys.argv[2:]]
 libs = [ctypes.CDLL(os.path.abspath(sp[0])) for sp in specs]
@@ -47,6 +51,12 @@ def params(o):
 
 ps = [params(o) for o in outs]
 dcode = 0 if dt == torch.float16 else 1
+wss = [None] * len(libs)
+if os.environ.get("AB_WS") == "1":
+    for i, lib in enumerate(libs):
+        lib.fa_fwd_gfx950_workspace_size.restype = ctypes.c_int64
+        n = lib.fa_fwd_gfx950_workspace_size(ctypes.byref(ps[i]), dcode, int(cfg["causal"]))
+        wss[i] = torch.empty(max(n, 256), dtype=torch.uint8, device=dev) if n > 0 else None
 
 
 def run(i, n):
@@ -55,6 +65,9 @@ def run(i, n):
         if cfg.get("W"):  # local-window configs: fa_fwd_gfx950_window
             rc = libs[i].fa_fwd_gfx950_window(ctypes.byref(ps[i]), dcode, int(cfg["causal"]),
                                               ctypes.c_int64(cfg["W"] - 1), ctypes.c_void_p(stream))
+        elif wss[i] is not None:  # AB_WS=1: the workspace the library asks for (key-split blocks)
+            rc = libs[i].fa_fwd_gfx950_ws(ctypes.byref(ps[i]), dcode, int(cfg["causal"]), ctypes.c_void_p(wss[i].data_ptr()),
+                                          ctypes.c_int64(wss[i].numel()), ctypes.c_void_p(stream))
         else:
             rc = libs[i].fa_fwd_gfx950(ctypes.byref(ps[i]), dcode, int(cfg["causal"]), ctypes.c_void_p(stream))
         assert rc == 0

@@ -21,9 +21,7 @@ if "--sweep" in sys.argv:  # where the layout pays: sequence length x one-round 
     shapes = [(f"B1 Hq{h}/{max(h // 4, 1)} S{s} bf16 ({h * ((s + 255) // 256)} blocks)", 1, h, max(h // 4, 1), s, torch.bfloat16)
               for s in (1024, 2048, 3072, 4096, 6144, 8192) for h in (4, 8, 16, 32, 64)
               if 64 <= h * ((s + 255) // 256) <= 256]
-modes = {"split": (1, None, 0), "zigzag": (0, None, 0), "plain": (0, 0, 0)}
-if "--pieces" in sys.argv:  # the same rule with 4 pieces per block (forced where the rule splits)
-    modes["split4"] = (1, None, 4)
+modes = {"split": (1, None), "zigzag": (0, None), "plain": (0, 0)}
 op = torch.ops.flash_attention.forward
 for name, b, hq, hkv, s, dt in shapes:
     q = torch.randn(b, hq, s, 128, device=dev, dtype=dt)
@@ -33,10 +31,9 @@ for name, b, hq, hkv, s, dt in shapes:
     res = {m: [] for m in modes}
     outs, lay = {}, {}
     for rep in range(7):
-        for mname, (sp, zz, pc) in modes.items():
+        for mname, (sp, zz) in modes.items():
             _debug.set_split(sp)
             _debug.set_zigzag(zz)
-            _debug.set_split_pieces(pc)
             outs[mname] = op(q, k, v, 128 ** -0.5, True)
             lay[mname] = _debug.last_layout()
             torch.cuda.synchronize()
@@ -50,10 +47,8 @@ for name, b, hq, hkv, s, dt in shapes:
             res[mname].append(flops * n / (a.elapsed_time(e) * 1e-3) / 1e12)
     _debug.set_split(None)
     _debug.set_zigzag(None)
-    _debug.set_split_pieces(None)
     med = {m: sorted(r)[len(r) // 2] for m, r in res.items()}
     d = (outs["split"].float() - outs["plain"].float()).abs().max().item()
     print(f"{name}: " + ", ".join(f"{m} ({lay[m]}) {med[m]:.1f}" for m in modes)
           + f" TF/s; split/zigzag x{med['split'] / med['zigzag']:.3f}, split/plain x{med['split'] / med['plain']:.3f}; "
-          + (f"split4/split x{med['split4'] / med['split']:.3f}; " if "split4" in med else "")
-          + f"max|split - plain| {d:.2e}", flush=True)
+          f"max|split - plain| {d:.2e}", flush=True)

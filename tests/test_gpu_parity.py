@@ -364,13 +364,12 @@ SPLIT = [  # (B, Hq, Hkv, Sq, Sk, D): causal launches whose 256-row blocks fit o
 ]
 
 
-@pytest.mark.parametrize("pieces", [2, 4])
 @pytest.mark.parametrize("shape", SPLIT, ids=[str(s) for s in SPLIT])
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16], ids=["f16", "bf16"])
-def test_key_split_causal_blocks(device, shape, dtype, pieces):
-    """Key-split causal blocks (fa_fwd_w4 "Key-split causal blocks": each block's key tiles in P
-    (2 or 4) pieces on as many workgroups, the last combining), knob 2 (always; the default rule
-    picks long one-round grids);
+def test_key_split_causal_blocks(device, shape, dtype):
+    """Key-split causal blocks (fa_fwd_w4 "Key-split causal blocks": each block's key tiles in two
+    pieces on two workgroups, the second combining), knob 2 (always; the default rule picks long
+    one-round grids);
     against the oracle, two launches bit-identical (the combine does not depend on which piece
     arrives second), any persistent grid size bit-identical, and close to the unsplit layout."""
     import flash_attention_cute_amd as m
@@ -382,7 +381,6 @@ def test_key_split_causal_blocks(device, shape, dtype, pieces):
     qd, kd, vd = q.to(device), k.to(device), v.to(device)
     _debug.set_knobs()
     _debug.set_split(2)
-    _debug.set_split_pieces(pieces)
     try:
         out = m.flash_attn_func(qd, kd, vd, causal=True)
         assert _debug.last_path() == "w4" and _debug.last_layout() == "split"
@@ -397,7 +395,6 @@ def test_key_split_causal_blocks(device, shape, dtype, pieces):
         torch.cuda.synchronize()
     finally:
         _debug.set_split()
-        _debug.set_split_pieces()
         _debug.set_zigzag()
     assert torch.equal(out, again) and torch.equal(out, small)
     check(out, q, k, v, d ** -0.5, True, dtype)
