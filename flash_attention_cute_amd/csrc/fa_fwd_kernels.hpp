@@ -190,13 +190,15 @@ __device__ __forceinline__ float sum_of_products(float a, float fa, float b, flo
 __device__ __forceinline__ void st_ws(u32x4 *p, const u32x4 v) {
     asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
-// four records 64 x 16 B apart (p, p + 64, p + 128, p + 192), landed
-__device__ __forceinline__ void ld_ws4(const u32x4 *p, u32x4 (&x)[4]) {
-    asm volatile("global_load_dwordx4 %0, %4, off sc1\n\tglobal_load_dwordx4 %1, %4, off offset:1024 sc1\n\t"
-                 "global_load_dwordx4 %2, %4, off offset:2048 sc1\n\tglobal_load_dwordx4 %3, %4, off offset:3072 sc1\n\t"
+// four records 64 x 16 B apart from each of pa and pb, landed (one round trip for two d-tiles)
+__device__ __forceinline__ void ld_ws8(const u32x4 *pa, const u32x4 *pb, u32x4 (&x)[4], u32x4 (&y)[4]) {
+    asm volatile("global_load_dwordx4 %0, %8, off sc1\n\tglobal_load_dwordx4 %1, %8, off offset:1024 sc1\n\t"
+                 "global_load_dwordx4 %2, %8, off offset:2048 sc1\n\tglobal_load_dwordx4 %3, %8, off offset:3072 sc1\n\t"
+                 "global_load_dwordx4 %4, %9, off sc1\n\tglobal_load_dwordx4 %5, %9, off offset:1024 sc1\n\t"
+                 "global_load_dwordx4 %6, %9, off offset:2048 sc1\n\tglobal_load_dwordx4 %7, %9, off offset:3072 sc1\n\t"
                  "s_waitcnt vmcnt(0)"
-                 : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3])
-                 : "v"(p)
+                 : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3]), "=&v"(y[0]), "=&v"(y[1]), "=&v"(y[2]), "=&v"(y[3])
+                 : "v"(pa), "v"(pb)
                  : "memory");
 }
 // two records (p, p + 64), landed
@@ -1954,36 +1956,41 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             }
         }
     };
-    // key-split blocks: the same stores of o * fm + pw * fo (pw: the partner piece's partial O of this
-    // block), one d-tile at a time to keep the live registers of the epilogue low. Two rounded
-    // products and their rounded sum -- no fma: the same bits whichever piece arrives second.
-    auto store_block_combined = [&](const int row, auto OBASE, const float l_tot, const u32x4 *pw, const float fm,
-                                    const float fo) {
-        constexpr int ob0 = decltype(OBASE)::value;
-        const float inv = (l_tot == 0.f) ? 1.f : 1.f / l_tot;
-        const int orow = row * os_ * 2;
+    // key-split blocks: the same stores of o * fm + pw * fo (pw: the partner piece's partial O of
+    // this wave's two blocks), one d-tile of both blocks per load round trip (each round trip to the
+    // write-through records costs microseconds under load: measured +1.4 to +3.2 % over one d-tile of
+    // one block per trip), registers for one d-tile only. Two rounded products and their rounded
+    // sum -- no fma: the same bits whichever piece arrives second.
+    auto store_both_combined = [&](const float *lt, const u32x4 *pw, const float *fm, const float *fo) {
+        const float inv0 = (lt[0] == 0.f) ? 1.f : 1.f / lt[0], inv1 = (lt[1] == 0.f) ? 1.f : 1.f / lt[1];
         static_for<DTL>([&](auto DD) {
             constexpr int dt = decltype(DD)::value;
-            f32x16 od = agpr_read16<ob0 + 16 * dt>();
-            u32x4 xs[4];
-            ld_ws4(pw + dt * 4 * 64 + lane, xs);
+            u32x4 xs[2][4];
+            ld_ws8(pw + dt * 4 * 64 + lane, pw + (DTL + dt) * 4 * 64 + lane, xs[0], xs[1]);
+            static_for<2>([&](auto XX) {
+                constexpr int X = decltype(XX)::value;
+                f32x16 od = agpr_read16<16 * DTL * X + 16 * dt>();
+                const float inv = X ? inv1 : inv0;
+                const int orow = (X ? r + rowb_c : r) * os_ * 2;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+                for (int q = 0; q < 4; ++q) {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) od[4 * q + e] = sum_of_products(od[4 * q + e], fm, __uint_as_float(xs[q][e]), fo);
-            }
+                    for (int e = 0; e < 4; ++e)
+                        od[4 * q + e] = sum_of_products(od[4 * q + e], fm[X], __uint_as_float(xs[X][q][e]), fo[X]);
+                }
 #pragma unroll
-            for (int gp = 0; gp < 4; gp += 2) {
-                const uint32_t a0 = DT::pack(od[4 * gp + 0] * inv, od[4 * gp + 1] * inv);
-                const uint32_t a1 = DT::pack(od[4 * gp + 2] * inv, od[4 * gp + 3] * inv);
-                const uint32_t b0 = DT::pack(od[4 * gp + 4] * inv, od[4 * gp + 5] * inv);
-                const uint32_t b1 = DT::pack(od[4 * gp + 6] * inv, od[4 * gp + 7] * inv);
-                const auto x0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
-                const auto x1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
-                const int d0 = dt * 32 + 8 * (gp + h);
-                __builtin_amdgcn_raw_buffer_store_b128((u32x4){x0[0], x1[0], x0[1], x1[1]}, orr,
-                                                       (kExactD || d0 < D) ? orow + 2 * d0 : 0x7ffffff0, 0, 0);
-            }
+                for (int gp = 0; gp < 4; gp += 2) {
+                    const uint32_t a0 = DT::pack(od[4 * gp + 0] * inv, od[4 * gp + 1] * inv);
+                    const uint32_t a1 = DT::pack(od[4 * gp + 2] * inv, od[4 * gp + 3] * inv);
+                    const uint32_t b0 = DT::pack(od[4 * gp + 4] * inv, od[4 * gp + 5] * inv);
+                    const uint32_t b1 = DT::pack(od[4 * gp + 6] * inv, od[4 * gp + 7] * inv);
+                    const auto x0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+                    const auto x1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+                    const int d0 = dt * 32 + 8 * (gp + h);
+                    __builtin_amdgcn_raw_buffer_store_b128((u32x4){x0[0], x1[0], x0[1], x1[1]}, orr,
+                                                           (kExactD || d0 < D) ? orow + 2 * d0 : 0x7ffffff0, 0, 0);
+                }
+            });
         });
     };
     FA_STAMP(s_masked_end);
@@ -2042,8 +2049,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                 fo[X] = so ? __builtin_amdgcn_exp2f(mo - mt) : 0.f;
                 lt[X] = pair_sum(sum_of_products(st[X].l, fm[X], __uint_as_float(s0[2 + X]), fo[X]));
             }
-            store_block_combined(r, IC<0>{}, lt[0], wsw, fm[0], fo[0]);
-            store_block_combined(r + rowb_c, IC<16 * DTL>{}, lt[1], wsw + 4 * DTL * 64, fm[1], fo[1]);
+            store_both_combined(lt, wsw, fm, fo);
         }
     }
 #ifdef FA_STAMPS
