@@ -39,6 +39,7 @@ import argparse
 import json
 import os
 import platform
+import statistics
 import sys
 import time
 from pathlib import Path
@@ -323,10 +324,12 @@ def load_traffic(config_key: str):
     return d.get("hbm_bytes_per_launch"), {"traffic_stale": False, "traffic_source": f"profiles/pmc_{config_key}.json"}
 
 
-def roofline(c, kern_ms: float, traffic, rank_flops=None, rank_bytes=None):
+def roofline(c, kern_ms: float, traffic, rank_flops=None, rank_bytes=None, median=None):
     """Roofline of the attention kernel: MFMA-bound for prefill (intensity ~2 kFLOP/B at S=4096),
     HBM-bound for decode (Sq = 1: one pass over K/V per q-head group). ``rank_*``: the work of the
-    launches timed (one rank's shard under --strong), default the whole config."""
+    launches timed (one rank's shard under --strong), default the whole config. ``achieved`` is the mean
+    over the timed launches; ``median`` = (median ms per launch, launches) of individually timed
+    launches (BASELINE.md's statistic), reported beside it as ``kernel_ms_median`` / ``frac_median``."""
     fl = flops(c) if rank_flops is None else rank_flops
     by = algo_bytes(c) if rank_bytes is None else rank_bytes
     gbs = by / (kern_ms * 1e-3) / 1e9
@@ -334,6 +337,10 @@ def roofline(c, kern_ms: float, traffic, rank_flops=None, rank_bytes=None):
     traffic, prov = traffic if isinstance(traffic, tuple) else (traffic, {})
     base = {"traffic": traffic, **prov, "kernel_ms": round(kern_ms, 4), "algorithmic_bytes": by,
             "algorithmic_flops": fl}
+    if median is not None:
+        med_ms, n_med = median
+        rate = by / (med_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if c["Sq"] == 1 else fl / (med_ms * 1e-3) / 1e12 / PEAK_TFLOPS
+        base.update({"kernel_ms_median": round(med_ms, 4), "median_launches": n_med, "frac_median": round(rate, 4)})
     if c["Sq"] == 1:
         return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gbs / HBM_PEAK_GBS, 4), "achieved_TFLOPs": round(tf, 3), **base}
@@ -520,6 +527,17 @@ def main() -> None:
         torch.cuda.synchronize()
         return time.perf_counter() - t0, a.elapsed_time(b) / n
 
+    def per_launch_median(fn, n):
+        """(median HIP-event ms of n launches of fn, each bracketed by its own event pair, n)."""
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+        torch.cuda.synchronize()
+        for a, b in evs:
+            a.record()
+            fn()
+            b.record()
+        torch.cuda.synchronize()
+        return statistics.median(a.elapsed_time(b) for a, b in evs), n
+
     main_step = layer_step if layer else step
     # Device warm-up: the MI355X ramps its clock over the first ~second of sustained load, so a
     # few warm-up steps leave the timed steps on a still-rising clock (C2: 1043 TFLOPS after 5
@@ -550,6 +568,9 @@ def main() -> None:
         dist.barrier()
     # the attention kernel alone (roofline): HIP events around the op's launches on the current stream
     kern_ms = step_ms if not layer else extra["layer"]["bare_op_ms"]
+    # BASELINE.md's statistic beside the mean: the median over >= 50 launches, each between its own
+    # event pair (after the timed region, so the pairs' gaps do not touch `value`)
+    kern_med_ms, n_med = per_launch_median(step, max(50, args.steps))
 
     (elapsed,) = reduce_max(world, elapsed)
 
@@ -597,7 +618,7 @@ def main() -> None:
         "roofline": roofline(c, kern_ms, load_traffic(args.config) if mode["whole_default_workload"] else
                              (None, {"traffic_source": None, "traffic_note": "launches differ from the profiled "
                                      "workload (a shard or another batch)"}),
-                             rank_flops=rank_flops, rank_bytes=rank_bytes),
+                             rank_flops=rank_flops, rank_bytes=rank_bytes, median=(kern_med_ms, n_med)),
         "cpu_baseline": None,
         **extra,
     }

@@ -55,6 +55,8 @@ def lib(debug: bool = False) -> ctypes.CDLL:
         lib.fa_debug_set_split.argtypes = [ctypes.c_int]
         lib.fa_debug_set_split.restype = None
         lib.fa_debug_last_zigzag.restype = ctypes.c_int
+        lib.fa_split_errors.argtypes = [ctypes.c_int]
+        lib.fa_split_errors.restype = ctypes.c_int64
         _libs[debug] = lib
     return _libs[debug]
 

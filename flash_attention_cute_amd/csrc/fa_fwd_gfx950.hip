@@ -7,6 +7,8 @@
 // fa_fwd_kernels.hpp and are instantiated by fa_inst.hip.
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
+
+#include <mutex>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -127,6 +129,79 @@ int64_t fa::device_cus() {
     return n;
 }
 
+int64_t fa::w4_grid_split(int64_t units) {
+    int64_t cap = device_cus();
+    if (fa::knobs().w4_grid > 0) cap = fa::knobs().w4_grid;
+    cap = cap < 8 ? 8 : cap / 8 * 8;
+    const int64_t n = 16 * ((units + 7) / 8);  // 2 pieces x ceil(units / 8) per XCD
+    return n < cap ? n : cap;
+}
+
+// Key-split counter areas (fa_launch.h split_sync_area): one per (device, stream), allocated and zeroed
+// the first time a key-split launch runs on that stream outside graph capture, never freed (a captured
+// graph keeps using the area its launches were given). The kernel's combining pieces zero their counters
+// again, so the area is zero between launches and no launch needs a memset. Streams of one device that
+// run key-split launches concurrently each get their own area.
+namespace {
+constexpr int64_t kSyncAreaBytes = 256 * 1024;  // 8192 blocks x 4 waves x 2 counters
+constexpr int kMaxAreas = 64;
+struct SyncArea {
+    int dev;
+    hipStream_t stream;
+    unsigned *ptr;
+};
+std::mutex g_sync_mu;
+SyncArea g_areas[kMaxAreas];
+int g_n_areas = 0;
+unsigned *g_split_err[64] = {};  // per device: hand-offs that timed out
+}  // namespace
+
+unsigned *fa::split_sync_area(hipStream_t stream, int64_t bytes, unsigned **err) {
+    *err = nullptr;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) != hipSuccess) return nullptr;
+    const bool capturing = cs != hipStreamCaptureStatusNone;
+    std::lock_guard<std::mutex> lk(g_sync_mu);
+    if (!g_split_err[dev] && !capturing) {  // (synchronous: ordered before every stream's later launches)
+        unsigned *e = nullptr;
+        if (hipMalloc(&e, 256) == hipSuccess) {
+            if (hipMemset(e, 0, 256) == hipSuccess && hipDeviceSynchronize() == hipSuccess) g_split_err[dev] = e;
+            else (void)hipFree(e);
+        }
+    }
+    *err = g_split_err[dev];
+    if (bytes > kSyncAreaBytes) return nullptr;
+    for (int i = 0; i < g_n_areas; ++i)
+        if (g_areas[i].dev == dev && g_areas[i].stream == stream) return g_areas[i].ptr;
+    if (capturing || g_n_areas >= kMaxAreas) return nullptr;
+    unsigned *a = nullptr;
+    if (hipMalloc(&a, kSyncAreaBytes) != hipSuccess) return nullptr;
+    if (hipMemset(a, 0, kSyncAreaBytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        (void)hipFree(a);
+        return nullptr;
+    }
+    g_areas[g_n_areas++] = {dev, stream, a};
+    return a;
+}
+
+extern "C" int64_t fa_split_errors(int reset) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    unsigned *e = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_sync_mu);
+        e = g_split_err[dev];
+    }
+    if (!e) return 0;
+    unsigned n = 0;
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(&n, e, sizeof(n), hipMemcpyDeviceToHost) != hipSuccess)
+        return 0;
+    if (reset && n) (void)hipMemset(e, 0, sizeof(unsigned));
+    return (int64_t)n;
+}
+
 int64_t fa::w4_grid(int64_t nwg) {
     int64_t cap = device_cus();
     if (fa::knobs().w4_grid > 0) cap = fa::knobs().w4_grid;
@@ -137,7 +212,7 @@ int64_t fa::w4_grid(int64_t nwg) {
     return nwg < cap ? nwg : cap;
 }
 
-// Diagnostic hook (not in include/fa_gfx950.h): device buffer of 12 u64 per wave of the next
+// Diagnostic hook (not in include/fa_gfx950.h): device buffer of 13 u64 per wave (17 with FA_STAMPS_FINE) of the next
 // launches; honoured only by a -DFA_STAMPS=1 build of the kernels (scripts/stamps.py).
 extern "C" void fa_debug_set_stamps(void *device_buffer) { g_stamps = (unsigned long long *)device_buffer; }
 
@@ -242,14 +317,16 @@ int dispatch(const fa_fwd_params *params, int dtype, int causal, void *ws, int64
         return causal ? launch_dec<fa::BF16, true>(p, a, ws, s) : launch_dec<fa::BF16, false>(p, a, ws, s);
     }
     fa::PathArgs xa = ranges;
-    if (ws && fa::use_split(p, causal != 0, ranges)) {  // key-split causal blocks (fa_launch.h use_split)
-        if (fa::split_ws_bytes(p) > ws_bytes)
-            return set_err(FA_ERR_INVALID_ARGUMENT, "workspace of %lld bytes is smaller than the %lld required",
-                           (long long)ws_bytes, (long long)fa::split_ws_bytes(p));
-        xa.split_sync = (unsigned *)ws;
+    // key-split causal blocks (fa_launch.h use_split) when the workspace holds their partials; a
+    // smaller one runs the blocks unsplit (zigzag), as without a workspace
+    if (ws && fa::use_split(p, causal != 0, ranges) && fa::split_ws_bytes(p) <= ws_bytes) {
         xa.split_ws = (float *)((char *)ws + fa::split_sync_bytes(p));
-        const hipError_t e = hipMemsetAsync(ws, 0, fa::split_sync_bytes(p), s);
-        if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "hipMemsetAsync failed: %s", hipGetErrorString(e));
+        xa.split_sync = fa::split_sync_area(s, fa::split_sync_bytes(p), &xa.split_err);
+        if (!xa.split_sync) {  // (graph capture before the stream's area exists: counters in the workspace)
+            xa.split_sync = (unsigned *)ws;
+            const hipError_t e = hipMemsetAsync(ws, 0, fa::split_sync_bytes(p), s);
+            if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "hipMemsetAsync failed: %s", hipGetErrorString(e));
+        }
     }
     if (dtype == FA_DTYPE_F16)
         return causal ? launch<fa::F16, true>(p, s, xa) : launch<fa::F16, false>(p, s, xa);

@@ -177,13 +177,15 @@ __device__ __forceinline__ float sum_of_products(float a, float fa, float b, flo
     asm volatile("" : "+v"(x), "+v"(y));
     return x + y;
 }
-// Key-split workspace accesses (the pieces of a block are paired on one XCD by fa_fwd_w4's work
-// order, for speed; correctness does not rest on it): every record store is a 16-B write-through
-// (sc1) store drained by its wave before the flag, the flag an agent-scope (sc1) store, the
-// counter an agent-scope atomic, and every load of a record or statistic an sc1 load (bypasses
-// this CU's L1) behind the poll. That is the placement-independent hand-off with no agent-scope
-// fence (a release / acquire fence writes back / invalidates the whole L2 of the XCD, the K/V lines
-// of every other workgroup included: measured, the layout ran at half speed with them). Inline asm
+// Key-split workspace accesses. The two pieces of a block run on ONE XCD: fa_fwd_w4's work order puts
+// both in the list of the XCD that blockIdx & 7 names, and the hardware deals workgroups to XCDs
+// round-robin by workgroup id (MI355X_MICROARCH "Workgroup dispatch"). The hand-off relies on that
+// shared L2: every record store is a 16-B write-through (sc1) store drained by its wave before the
+// flag, the flag an agent-scope (sc1) store, the counter an agent-scope atomic, and every load of a
+// record or statistic an sc1 load (bypasses this CU's L1) behind the poll -- with no agent-scope fence
+// and no buffer_wbl2 / buffer_inv, which write back / invalidate the whole L2 of the XCD, the K/V lines
+// of every other workgroup included (measured: the layout ran at half speed with them). Pieces on two
+// XCDs would need them. A poll that times out is counted (fa_split_errors). Inline asm
 // (the builtin forms cost the D=128 causal kernels a spilled VGPR), so: the loads and their wait in
 // ONE statement with early-clobber outputs (hipcc counts no asm load), and every 16-B store ends in
 // s_nop 1 (hipcc may otherwise overwrite its data registers before the store has read them).
@@ -620,16 +622,6 @@ __device__ __forceinline__ void agpr_mfma(const u32x4 &a, const u32x4 &b) {
     FA_CASE(0) FA_CASE(16) FA_CASE(32) FA_CASE(48) FA_CASE(64) FA_CASE(80) FA_CASE(96) FA_CASE(112)
 #undef FA_CASE
 }
-#ifdef FA_EXP_CZERO
-// (experiment only) a[BASE..BASE+15] = A.B with C = 0
-template <bool kF16, int BASE>
-__device__ __forceinline__ void agpr_mfma_c0(const u32x4 &a, const u32x4 &b) {
-    if constexpr (kF16)
-        asm volatile("v_mfma_f32_32x32x16_f16 a[%2:%3], %0, %1, 0" ::"v"(a), "v"(b), "n"(BASE), "n"(BASE + 15) : "memory");
-    else
-        asm volatile("v_mfma_f32_32x32x16_bf16 a[%2:%3], %0, %1, 0" ::"v"(a), "v"(b), "n"(BASE), "n"(BASE + 15) : "memory");
-}
-#endif
 template <int DTL, bool kBlockB>
 __device__ __forceinline__ void agpr_scale(const float alpha) {
     if constexpr (DTL == 4) {
@@ -719,6 +711,9 @@ __device__ __forceinline__ void mfma_sq(const bool first, f32x16 &acc, const u32
 // enforced by _asm_check rule R3). (FA_DRAIN21: the 21 of rounds 1-3, for A/B.)
 __device__ __forceinline__ void s_ready(f32x16 &s0, f32x16 &s1) { asm volatile(FA_DRAIN_NOPS : "+v"(s0), "+v"(s1)); }
 __device__ __forceinline__ void mfma_drain() { asm volatile(FA_DRAIN_NOPS ::: "memory"); }
+__device__ __forceinline__ void s_ready4(f32x16 &s0, f32x16 &s1, f32x16 &s2, f32x16 &s3) {
+    asm volatile(FA_DRAIN_NOPS : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3));
+}
 
 #define FA_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 // s_waitcnt lgkmcnt(0) alone (gfx9 encoding: vmcnt 63, expcnt 7, lgkmcnt 0)
@@ -741,6 +736,29 @@ __device__ __forceinline__ void mask_pair(f32x16 &s0, f32x16 &s1, const int e, c
         : "+v"(x0), "+v"(x1), "=&s"(m)
         : "v"(e), "n"(c), "n"(c + 32), "v"(neg)
         : "vcc");
+    s0[I] = x0;
+    s1[I] = x1;
+}
+
+// The same with a local window: score c is visible iff f <= c <= e (f: the lane's first visible key
+// minus key0 + 4h), so both compares and their AND per score (two chains: VCC and SGPR pairs)
+template <int I>
+__device__ __forceinline__ void mask_pair_win(f32x16 &s0, f32x16 &s1, const int e, const int f, const float neg) {
+    constexpr int c = (I & 3) + 8 * (I >> 2);
+    float x0 = s0[I], x1 = s1[I];
+    uint64_t m0, m1;
+    asm volatile(
+        "v_cmp_le_i32_e32 vcc, %5, %4\n\t"
+        "v_cmp_ge_i32_e64 %2, %5, %8\n\t"
+        "v_cmp_le_i32_e64 %3, %6, %4\n\t"
+        "s_and_b64 vcc, vcc, %2\n\t"
+        "v_cmp_ge_i32_e64 %2, %6, %8\n\t"
+        "v_cndmask_b32_e64 %0, %7, %0, vcc\n\t"
+        "s_and_b64 %3, %3, %2\n\t"
+        "v_cndmask_b32_e64 %1, %7, %1, %3"
+        : "+v"(x0), "+v"(x1), "=&s"(m0), "=&s"(m1)
+        : "v"(e), "n"(c), "n"(c + 32), "v"(neg), "v"(f)
+        : "vcc", "scc");
     s0[I] = x0;
     s1[I] = x1;
 }
@@ -875,9 +893,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #define FA_STAMP(v) const uint32_t v = (uint32_t)__builtin_amdgcn_s_memtime()
 #ifdef FA_STAMPS_FINE  // (finer split: phase 2 at the ends of its quarters, phase 1 at its middle)
     uint32_t st_f[4] = {0, 0, 0, 0}, st_fa[4] = {0, 0, 0, 0};
-#define FA_STAMP_W 16
+#define FA_STAMP_W 17
 #else
-#define FA_STAMP_W 12
+#define FA_STAMP_W 13
 #endif
 #else
     (void)stamps;
@@ -1353,12 +1371,14 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // boundary: A/B C2 +0.9 %, C4 +0.5 %, C5 +1.1 %, bit-identical (profiles/r4_ab_batch1.log)
     u32x4 va_pre[DTL];
     // AD (A-dead tiles, causal diagonal): bit 0 = block A has no visible score in this tile (its S
-    // MFMAs are skipped), bit 1 = nor in the previous tile (its late softmax units are skipped)
+    // MFMAs are skipped), bit 1 = nor in the previous tile (its late softmax units are skipped);
+    // bit 2 = read phase 2's first V^T fragments into va_pre (with SM2)
     auto phase1 = [&](const char *K, auto PAR, auto SM2, auto DMA, const rsrc_t &kq, const rsrc_t &vq, auto AD)
         __attribute__((always_inline)) {
         constexpr int c = decltype(PAR)::value, pr = c ^ 1;
         constexpr bool do_sm = decltype(SM2)::value, do_dma = decltype(DMA)::value;
         constexpr bool sdead = decltype(AD)::value & 1, pdead = decltype(AD)::value & 2;
+        constexpr bool vpre = decltype(AD)::value & 4;
         u32x4 kf[2][2];  // [buffer][key half]
 #pragma unroll
         for (int x = 0; x < 2; ++x) kf[0][x] = *(const u32x4 *)(K + x * 32 * RB + k_addr[0]);
@@ -1404,7 +1424,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #endif
                 }
             }
-            if constexpr (do_sm && ks == KS - 1 && i < DTL) {
+            if constexpr (do_sm && vpre && ks == KS - 1 && i < DTL) {
                 static_for<2>([&](auto E) {
                     constexpr int n = 2 * i + decltype(E)::value;
                     const u32x2 x = tr_read(K + (2 + pr - c) * T + (n & 1) * 8 * RB + v_addr[n >> 1]);
@@ -1497,13 +1517,13 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         return true;
     }(), "phase-2 softmax schedule");
     // AD: bit 0 = block A has no visible score in tile cs (its early softmax units are skipped),
-    // bit 1 = nor in tile cp (its P.V MFMAs are skipped: P is 0)
-    auto phase2 = [&](const char *V, auto PPV, auto PSM, auto SM1, auto AD, const bool czf = false)
-        __attribute__((always_inline)) {
-        (void)czf;
+    // bit 1 = nor in tile cp (its P.V MFMAs are skipped: P is 0); bit 2 = the first V^T fragments
+    // are in va_pre (with SM1)
+    auto phase2 = [&](const char *V, auto PPV, auto PSM, auto SM1, auto AD) __attribute__((always_inline)) {
         constexpr int cp = decltype(PPV)::value, cs = decltype(PSM)::value;
         constexpr bool do_sm = decltype(SM1)::value;
         constexpr bool sdead = decltype(AD)::value & 1, pdead = decltype(AD)::value & 2;
+        constexpr bool vpre = decltype(AD)::value & 4;  // (phase 1 read the first V^T fragments)
         u32x4 va[2][DTL];
         auto rd = [&](const int kk, const int n, u32x4 *dst) {
             const int rowoff = ((kk >> 1) * 32 + (kk & 1) * 16) * RB + (n & 1) * 8 * RB;
@@ -1516,7 +1536,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             dst[n >> 1][2 * (n & 1)] = x[0];
             dst[n >> 1][2 * (n & 1) + 1] = x[1];
         };
-        if constexpr (do_sm) {  // (read in phase 1 of the same iteration)
+        if constexpr (do_sm && vpre) {  // (read in phase 1 of the same iteration)
 #pragma unroll
             for (int n = 0; n < DTL; ++n) va[0][n] = va_pre[n];
         } else {
@@ -1532,14 +1552,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #ifndef FA_EXP_NOLGKM2
             if constexpr (kk > 0 && i == 0) __builtin_amdgcn_s_waitcnt(kLgkm0);
 #endif
-#ifdef FA_EXP_CZERO
-            if constexpr (!(pdead && X == 0)) {
-                if (kk == 0 && czf) agpr_mfma_c0<F, X * 16 * DTL + 16 * dt>(va[kk & 1][dt], P[cp][4 * X + kk]);
-                else agpr_mfma<F, X * 16 * DTL + 16 * dt, true>(va[kk & 1][dt], P[cp][4 * X + kk]);
-            }
-#else
             if constexpr (!(pdead && X == 0)) agpr_mfma<F, X * 16 * DTL + 16 * dt, true>(va[kk & 1][dt], P[cp][4 * X + kk]);
-#endif
             FA_SCHED_FENCE();  // (see phase 1)
             if constexpr (kk + 1 < 4 && i < DTL) {
 #if defined(FA_EXP_HALFLDS) || defined(FA_EXP_HALFV)  // (timing experiment, as in phase 1: half the V^T reads)
@@ -1628,7 +1641,10 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         return rows >= kBlockN ? full : slab_bytes(rows, stride, D);
     };
 
-    stage_k(j_lo, 0);  // the first block's first K tile (its Q is in flight above)
+    // Tile parity: a block's first tile j_lo runs with parity 1 (its own iteration, iter_first), the
+    // pipelined tiles j > j_lo with parity (j - j_lo - 1) & 1; parity c = K ring slot c, V slot c,
+    // S[c], P[c].
+    stage_k(j_lo, 1);  // the first block's first K tile (its Q is in flight above)
     for (;;) {
     // ---- block prologue: Q and K_0 of this block are in flight ------------------------------
 #ifdef FA_STAMPS
@@ -1653,30 +1669,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         st[X].nmsc = -5.77f;
 #endif
     }
-#ifdef FA_EXP_CZERO
-    // (round-3 experiment rebuilt for the analysis in DESIGN.md: no O zeroing here; the block's first
-    // UNMASKED iteration writes O with C = 0 P.V MFMAs instead -- a block whose first iteration is a
-    // masked one (causal first q-tiles, windows) then accumulates into the previous block's O. Gate:
-    // _asm_check rule R5 rejects this build.)
-    bool cz_first = true;
-#else
     if constexpr (DTL == 4) fa_agpr_zero_4(); else fa_agpr_zero_2();
-#endif
-    // tile -1 of the pipeline is empty: its S = kNeg gives P = 0, and its P.V reads V slot 1,
-    // zeroed here so that 0 * V stays 0 (the previous block's V may hold non-finite values).
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        S[1][1][i] = kNeg;
-        S[1][3][i] = kNeg;
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) P[1][i] = (u32x4){0, 0, 0, 0};
-    __syncthreads();  // every wave is past the previous block's reads of V slot 1
-    {
-        constexpr int per_thread = T / 256 / 16;
-#pragma unroll
-        for (int i = 0; i < per_thread; ++i) *(u32x4 *)(lds + KV0 + 3 * T + (i * 256 + tid) * 16) = (u32x4){0, 0, 0, 0};
-    }
+    // (no pipeline fill: the block's first tile runs its own iteration without the P.V and late
+    // softmax of an empty tile -1, iter_first below)
     // Q, K_0 landed. After the first block the previous block's O stores were issued after these
     // loads: leave them in flight (vmcnt counts stores too, in issue order)
     if (rnd == 0) dma_wait(); else __builtin_amdgcn_s_waitcnt(vmcnt_enc(kOStores));
@@ -1703,14 +1698,11 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             static_for<16>([&](auto I) { mask_pair<decltype(I)::value>(s0, s1, e, neg); });
         } else {  // and keys left of the row's window
             const int row = row0 + r;
-            const int lim = kCausal ? min(Sk - 1, row + diag) : Sk - 1;
-            const int lo = row + diag - wl;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int kk = key0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                if (kk > lim || kk < lo) s0[i] = kNeg;
-                if (kk + 32 > lim || kk + 32 < lo) s1[i] = kNeg;
-            }
+            const int e = (kCausal ? min(Sk - 1, row + diag) : Sk - 1) - key0 - 4 * h;
+            const int f = row + diag - wl - key0 - 4 * h;
+            float neg = kNeg;
+            asm volatile("" : "+v"(neg));
+            static_for<16>([&](auto I) { mask_pair_win<decltype(I)::value>(s0, s1, e, f, neg); });
         }
     };
     // does tile key0 hold a hidden score of rows row0..row0+31 (wave-uniform)? keys past the first
@@ -1719,12 +1711,39 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         const int lim = kCausal ? min(Sk - 1, row0 + diag) : Sk - 1;
         return key0 + kBlockN - 1 > lim || (wl >= 0 && key0 < row0 + 31 + diag - wl);
     };
+    // the first softmax half of a block's first tile on its own (iter FIRST: no P.V to pair it with;
+    // AD bit 0: block A dead)
+    auto sm1_first = [&](auto PAR, auto AD) __attribute__((always_inline)) {
+        constexpr int c = decltype(PAR)::value;
+        constexpr int X0 = (decltype(AD)::value & 1) ? 1 : 0;
+        static_for<2>([&](auto XX) {
+            constexpr int X = decltype(XX)::value;
+            if constexpr (X >= X0) {
+                static_for<16>([&](auto M) { u_max(c, X, decltype(M)::value); });
+                u_dec(c, X, 0);
+                u_dec(c, X, 1);
+                static_for<kV0>([&](auto VV) {  // the early scores (the late ones: the next tile's phase 1)
+                    constexpr int q = decltype(VV)::value;
+                    u_exp(c, X, q >> 4, q & 15);
+                    u_fin(c, X, q >> 4, q & 15);
+                });
+            }
+        });
+    };
     // MASKED: 0 = no masked score, 1 = masked (diagonal / tail / window), 2 = masked and block A
-    // dead in tile j (no row of any wave's block A sees a key of it), 3 = A dead in tiles j and j-1
-    auto iter = [&](const int j, auto PAR, auto MASKED) __attribute__((always_inline)) {
+    // dead in tile j (no row of any wave's block A sees a key of it), 3 = A dead in tiles j and j-1.
+    // FIRST: the block's first tile j_lo (parity 1). The pipeline is not filled with an empty tile
+    // -1: phase 1 computes S(j_lo) and issues the DMA of K_{j_lo+1} and V_{j_lo} with no late softmax
+    // beside it, and "phase 2" is the first softmax half of j_lo alone (no P.V of a tile -1: 32 MFMAs
+    // of zeros and their V^T reads in rounds 1-4, and the zeroed V slot behind them).
+    auto iter = [&](const int j, auto PAR, auto MASKED, auto FIRST) __attribute__((always_inline)) {
         constexpr int c = decltype(PAR)::value, pr = c ^ 1;
         constexpr int mk = decltype(MASKED)::value;
-        using AD = IC<mk == 2 ? 1 : mk == 3 ? 3 : 0>;
+        constexpr bool first = decltype(FIRST)::value;
+        static_assert(!first || (c == 1 && mk != 3), "first tile: parity 1, no previous tile");
+        // (bit 2: phase 2's first V^T fragments read in phase 1 -- unmasked tiles only: in a masked one
+        // they would stay live through the mask step, where the causal kernels have no VGPR to spare)
+        using AD = IC<(mk == 2 ? 1 : mk == 3 ? 3 : 0) | (mk == 0 ? 4 : 0)>;
         if constexpr (mk >= 2) {  // block A takes no decision and adds no row sum in tile j
             st[0].rmask = 0;
             st[0].t = 0.f;
@@ -1737,12 +1756,14 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #if defined(FA_EXP_NOSM)
         phase1(lds + KV0 + c * T, PAR, IC<0>{}, IC<1>{}, kq, vq, AD{});
 #elif defined(FA_EXP_NODMA)
-        phase1(lds + KV0 + c * T, PAR, IC<1>{}, IC<0>{}, kq, vq, AD{});
+        phase1(lds + KV0 + c * T, PAR, IC<!first>{}, IC<0>{}, kq, vq, AD{});
 #else
-        phase1(lds + KV0 + c * T, PAR, IC<1>{}, IC<1>{}, kq, vq, AD{});
+        phase1(lds + KV0 + c * T, PAR, IC<!first>{}, IC<1>{}, kq, vq, AD{});
 #endif
         kp += step_k;
         vp += step_v;
+        // the first tile's softmax reads S right after its MFMAs (no P.V MFMAs in between)
+        if constexpr (first) s_ready4(S[c][0], S[c][1], S[c][2], S[c][3]);
 #ifndef FA_EXP_NOMASK  // (timing experiment of the stamps build only: no mask step, wrong results)
         if constexpr (mk != 0) {  // diagonal / tail tile: mask S before phase 2
             // (per wave and block: only where some score of its 32 rows is hidden; on a causal
@@ -1750,36 +1771,39 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             const int key0 = j * kBlockN;
             if constexpr (mk == 1) {
                 if (hides(mw, key0)) {
-                    s_ready(S[c][0], S[c][1]);
+                    if constexpr (!first) s_ready(S[c][0], S[c][1]);
                     mask(S[c][0], S[c][1], mw, key0);
                 }
             }
             if (hides(mw + rowB, key0)) {
-                s_ready(S[c][2], S[c][3]);
+                if constexpr (!first) s_ready(S[c][2], S[c][3]);
                 mask(S[c][2], S[c][3], mw + rowB, key0);
             }
         }
 #endif
         FA_STAMP(sb);
+        if constexpr (first) {
+            sm1_first(PAR, AD{});
+            rescale(true);  // (O holds no P.V yet: l only)
+        } else {
 #if defined(FA_EXP_NOSM)
-        phase2(lds + KV0 + (2 + pr) * T, IC<pr>{}, PAR, IC<0>{}, AD{});
+            phase2(lds + KV0 + (2 + pr) * T, IC<pr>{}, PAR, IC<0>{}, AD{});
 #else
-#ifdef FA_EXP_CZERO
-        phase2(lds + KV0 + (2 + pr) * T, IC<pr>{}, PAR, IC<1>{}, AD{}, mk == 0 && cz_first);
-        if constexpr (mk == 0) cz_first = false;
-#else
-        phase2(lds + KV0 + (2 + pr) * T, IC<pr>{}, PAR, IC<1>{}, AD{});
+            phase2(lds + KV0 + (2 + pr) * T, IC<pr>{}, PAR, IC<1>{}, AD{});
 #endif
-#endif
-        rescale(j == j_lo);
+            rescale(false);
+        }
         FA_STAMP(sc_);
         dma_wait();  // K_{j+1}, V_j landed
         FA_STAMP(sd);
         __syncthreads();
 #ifdef FA_STAMPS
         const uint32_t se = (uint32_t)__builtin_amdgcn_s_memtime();
+        if constexpr (first) st_acc[5] += se - sa;  // (the first tile: its own record field)
 #ifdef FA_STAMPS_MASKED  // (diagnostic: the tile columns of the record count masked tiles only)
-        if constexpr (mk != 0)
+        if constexpr (mk != 0 && !first)
+#else
+        if constexpr (!first)
 #endif
         {
             st_acc[0] += sb - sa;
@@ -1799,9 +1823,10 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // every tile runs pipelined: first the tiles without a masked score, then (a second loop, so
     // the hot loop carries no mask branch) the diagonal / tail tiles with a mask step between the
     // phases. The debug variant (dbg & 1) runs all tiles through the plain body below instead.
-    // Tile j runs with parity (j - j_lo) & 1 (ring slots and S / P registers). A local window adds
-    // a leading run of masked tiles [j_lo, j_um), rounded up to an even count so the unmasked loop
-    // starts on parity 0.
+    // The first tile j_lo runs alone (iter FIRST, parity 1); tile j > j_lo runs with parity
+    // (j - jb) & 1, jb = j_lo + 1 (ring slots and S / P registers). A local window adds a leading
+    // run of masked tiles [jb, j_um), rounded up to an even count so the unmasked loop starts on
+    // parity 0.
 #ifdef FA_DEBUG_VARIANTS
     const int n_loop = (dbg & 1) ? j_lo : n_end;
 #else
@@ -1809,19 +1834,6 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     const int n_loop = n_end;
 #endif
     const int n_unm = min(n_pipe, n_loop);
-    int j = j_lo;  // the next tile
-    if (j_um > j_lo) {
-        const int e = min(j_um + ((j_um - j_lo) & 1), n_loop);
-        for (int t = j; t < e; t += 2) {
-            iter(t, IC<0>{}, IC<1>{});
-            if (t + 1 < e) iter(t + 1, IC<1>{}, IC<1>{});
-        }
-        j = max(j, e);
-    }
-    for (int t = j; t < n_unm; t += 2) {
-        iter(t, IC<0>{}, IC<0>{});
-        if (t + 1 < n_unm) iter(t + 1, IC<1>{}, IC<0>{});
-    }
     // causal: the tiles from jA on hold no visible score of any wave's block A (its rows are the
     // workgroup's first half, m0 .. m0 + kRowB - 1): they run B only (MASKED 2, then 3)
     int jA = n_loop;
@@ -1830,22 +1842,43 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         const int x = min(Sk - 1, m0 + kRowB - 1 + diag);
         jA = x < 0 ? 0 : x / kBlockN + 1;
     }
+    const int jb = j_lo + 1;
+    int j = jb;  // the next tile after the first
+    // (the first tile computes block A even where no row of it sees a key -- key-split second pieces
+    // of the first q-tiles, Sq > Sk: its scores are masked; the A-dead tiles after it run MASKED 2, 3)
+    if (j_lo < n_loop) {
+        if (j_lo < j_um || j_lo >= n_unm) iter(j_lo, IC<1>{}, IC<1>{}, IC<true>{});
+        else iter(j_lo, IC<1>{}, IC<0>{}, IC<true>{});
+    }
     {
+        if (j_um > j) {
+            const int e = min(j_um + ((j_um - j) & 1), n_loop);
+            for (int t = j; t < e; t += 2) {
+                iter(t, IC<0>{}, IC<1>{}, IC<false>{});
+                if (t + 1 < e) iter(t + 1, IC<1>{}, IC<1>{}, IC<false>{});
+            }
+            j = max(j, e);
+        }
+        for (int t = j; t < n_unm; t += 2) {
+            iter(t, IC<0>{}, IC<0>{}, IC<false>{});
+            if (t + 1 < n_unm) iter(t + 1, IC<1>{}, IC<0>{}, IC<false>{});
+        }
         j = max(j, n_unm);
         const int j0 = j, jm = min(max(jA, j), n_loop);
-        if (((j - j_lo) & 1) && j < jm) iter(j++, IC<1>{}, IC<1>{});
+        if (((j - jb) & 1) && j < jm) iter(j++, IC<1>{}, IC<1>{}, IC<false>{});
         for (; j < jm; j += 2) {
-            iter(j, IC<0>{}, IC<1>{});
-            if (j + 1 < jm) iter(j + 1, IC<1>{}, IC<1>{});
+            iter(j, IC<0>{}, IC<1>{}, IC<false>{});
+            if (j + 1 < jm) iter(j + 1, IC<1>{}, IC<1>{}, IC<false>{});
         }
         j = max(j0, jm);  // (the pair loop may step past jm)
         if constexpr (kCausal) {
+            // (j > jA when the first tile or a window's leading run is past jA: they computed block A)
             if (j < n_loop) {
-                if ((j - j_lo) & 1) iter(j, IC<1>{}, IC<2>{}); else iter(j, IC<0>{}, IC<2>{});
+                if ((j - jb) & 1) iter(j, IC<1>{}, IC<2>{}, IC<false>{}); else iter(j, IC<0>{}, IC<2>{}, IC<false>{});
                 ++j;
             }
             for (; j < n_loop; ++j) {
-                if ((j - j_lo) & 1) iter(j, IC<1>{}, IC<3>{}); else iter(j, IC<0>{}, IC<3>{});
+                if ((j - jb) & 1) iter(j, IC<1>{}, IC<3>{}, IC<false>{}); else iter(j, IC<0>{}, IC<3>{}, IC<false>{});
             }
         }
     }
@@ -1854,12 +1887,12 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #ifdef FA_DEBUG_VARIANTS
     // ---- debug variant: every tile masked, not pipelined -----------------------------------
     if (n_loop < n_end) {
-        stage_v(n_loop, (n_loop - j_lo) & 1);  // the pipeline fetched V one tile late; catch up first
+        stage_v(n_loop, (n_loop - j_lo + 1) & 1);  // the pipeline fetched V one tile late; catch up first
         dma_wait();
         __syncthreads();
     }
     for (int j = n_loop; j < n_end; ++j) {
-        const int sl = (j - j_lo) & 1;
+        const int sl = (j - j_lo + 1) & 1;  // (K_{j_lo} is in slot 1)
         if (j + 1 < n_end) {
             stage_k(j + 1, sl ^ 1);
             stage_v(j + 1, sl ^ 1);
@@ -1903,7 +1936,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         } else if (!rope_q) {
             load_q();
         }
-        stage_k(j_lo, 0);
+        stage_k(j_lo, 1);
         if (q_in_agpr) q_from_lds();
     }
     // drain the last pipelined tile: softmax half 2 and P.V
@@ -1915,10 +1948,10 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     if (n_loop > jlo_c) {  // (set_block above moved j_lo to the next block)
         if (kCausal && last_dead) {
             if constexpr (kCausal) {
-                if ((n_loop - 1 - jlo_c) & 1) drain(IC<1>{}, IC<2>{}); else drain(IC<0>{}, IC<2>{});
+                if ((n_loop - jlo_c) & 1) drain(IC<1>{}, IC<2>{}); else drain(IC<0>{}, IC<2>{});
             }
         } else {
-            if ((n_loop - 1 - jlo_c) & 1) drain(IC<1>{}, IC<0>{}); else drain(IC<0>{}, IC<0>{});
+            if ((n_loop - jlo_c) & 1) drain(IC<1>{}, IC<0>{}); else drain(IC<0>{}, IC<0>{});
         }
     }
     FA_STAMP(s_pipe_end);
@@ -2029,12 +2062,24 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (every lane's records written through before the flag)
             if (lane == 0) __hip_atomic_store(sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-            if (lane == 0) {  // (bounded, ~1 s: a protocol bug ends in a wrong result, never in a hang)
+            // bounded poll (~1 s), so a protocol failure never hangs the GPU; a timeout is counted in
+            // the device's error counter (fa_split_errors) -- the rows it combines are wrong
+            uint32_t seen = 1;
+            if (lane == 0) {
+                seen = 0;
                 for (int it = 0; it < (1 << 22); ++it) {
-                    if (__hip_atomic_load(sync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+                    if (__hip_atomic_load(sync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+                        seen = 1;
+                        break;
+                    }
                     __builtin_amdgcn_s_sleep(8);
                 }
+                if (!seen && xa.split_err) __hip_atomic_fetch_add(xa.split_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // both pieces are past their last access to the pair: zero it for the next launch
+                __hip_atomic_store(sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
+            (void)seen;
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: loads stay below the poll)
             u32x4 s0, s1;
             ld_ws2(stats + lane, s0, s1);
@@ -2059,7 +2104,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         const unsigned long long rt_end = __builtin_amdgcn_s_memrealtime();
         if (stamps && lane == 0) {
             // per Q block: [total, p1, p2+rescale, dma wait, barrier, tiles, drain (+ next block's
-            //  prefetch issue), prologue, epilogue, realtime (100 MHz ticks), start time, xcc]
+            //  prefetch issue), prologue, epilogue, realtime (100 MHz ticks), start time, xcc, (FINE:
+            //  4 sub-phase fields), first tile]
             unsigned long long *o = stamps + ((size_t)blk_c * 4 + wave) * FA_STAMP_W;
             o[0] = s_end - st_t0;
             for (int i = 0; i < 5; ++i) o[1 + i] = st_acc[i];
@@ -2073,6 +2119,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #pragma unroll
             for (int i = 0; i < 4; ++i) o[12 + i] = st_fa[i];
 #endif
+            o[FA_STAMP_W - 1] = st_acc[5];  // the block's first tile (iter FIRST)
         }
     }
 #endif
@@ -2115,7 +2162,8 @@ int launch_one(const fa_fwd_params &p, const PathArgs &xa, hipStream_t stream) {
     else
 #endif
         // persistent: about one workgroup per CU (the kernel walks the Q blocks itself)
-        hipLaunchKernelGGL((fa_fwd_w4<DT, C, kD, kExact>), dim3((uint32_t)w4_grid(nwg)), dim3(256), 0, stream, p,
+        hipLaunchKernelGGL((fa_fwd_w4<DT, C, kD, kExact>),
+                           dim3((uint32_t)(xz.split_ws ? w4_grid_split(nwg / 2) : w4_grid(nwg))), dim3(256), 0, stream, p,
                            (int)n_qtiles, variant == 2 ? 1 : 0, stamp_buffer(), xz);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "HIP launch failed: %s", hipGetErrorString(e));

@@ -92,7 +92,8 @@ int64_t device_cus();
 // block runs as two pieces over the two halves of its key tiles, on two workgroups; the piece that
 // finishes first leaves its unnormalised O and row statistics in split_ws, the second combines
 // them with its own and stores O (fa_fwd_w4 "Key-split causal blocks"). split_sync: per (block,
-// wave) [arrivals, ready] counters, zeroed by the dispatcher before the launch.
+// wave) [arrivals, ready] counters, zero at the launch; the combining piece zeroes its pair again
+// (split_sync_area). split_err: the device's count of hand-offs that timed out (or nullptr).
 struct PathArgs {
     const void *cos;
     const void *sin;
@@ -105,6 +106,7 @@ struct PathArgs {
     int zigzag;
     float *split_ws;
     unsigned *split_sync;
+    unsigned *split_err;
 };
 
 // Whether a prefill launch runs zigzag Q blocks, and its logical q-tile count (blocks per (batch,
@@ -144,6 +146,16 @@ inline int64_t split_sync_bytes(const fa_fwd_params &p) { return (split_blocks(p
 inline int64_t split_ws_bytes(const fa_fwd_params &p) {
     return split_sync_bytes(p) + split_blocks(p) * 4 * split_wave_floats(p.headdim) * 4;
 }
+
+// The key-split counters of launches on `stream` of the current device: a device area allocated and
+// zeroed once (the kernel leaves it zeroed), or nullptr when `bytes` exceed it or the stream is capturing
+// a graph before the area exists (the caller then zeroes counters in its workspace). *err: the device's
+// hand-off error counter (nullptr under capture before it exists).
+unsigned *split_sync_area(hipStream_t stream, int64_t bytes, unsigned **err);
+// workgroups of a key-split launch over `units` plain blocks (2 pieces each): every XCD gets a workgroup
+// per piece of its units when that fits the grid cap (pieces are dealt to XCDs by unit, so 2 * units
+// workgroups could leave some XCD short and run both pieces of a block on one workgroup)
+int64_t w4_grid_split(int64_t units);
 
 // launch one (dtype, causal, head-dim tile, exact head dim) instantiation on `stream`
 template <class DT, bool C, int kD, bool kExact>

@@ -84,6 +84,16 @@ def flash_attn_func(q, k, v, softmax_scale=None, causal=False):
 # ---------------------------------------------------------------------------------------------
 # variable-length (packed) sequences -- no reference counterpart (reference README.md:18 TODO)
 # ---------------------------------------------------------------------------------------------
+def split_errors(reset: bool = False) -> int:
+    """Key-split hand-offs on the current device that timed out since the last reset (include/fa_gfx950.h
+    ``fa_split_errors``): a causal block split over two workgroups whose second piece did not see its
+    partner's partial result within ~1 s, so its rows are wrong. 0 in a healthy run; one host
+    synchronisation."""
+    from . import _debug
+
+    return int(_debug.lib().fa_split_errors(1 if reset else 0))
+
+
 def _bottom_right_causal(sq: int, sk: int, device) -> torch.Tensor:
     """[sq, sk] bool, True = visible: key n is visible to query m iff n <= m + sk - sq
     (the kernel's causal convention, reference csrc/mask.cuh:37-39)."""

@@ -23,6 +23,7 @@ csrc/flash_attention_api.cpp), ``attn.transpose(1, 2).reshape(B, S, -1)`` is cop
 """
 from __future__ import annotations
 
+import weakref
 from typing import NamedTuple, Optional, Tuple
 
 import torch
@@ -152,10 +153,15 @@ def lower_mask(attention_mask: Optional[torch.Tensor], sq: int, sk: int, causal:
         own = torch.where(a, n_[None, None], -1).amax(2)  # [B, Sq] the last key each row attends
         if causal:
             # real rows: own key = offset + row; padding rows attend only earlier keys (right padding,
-            # holes) or none (left padding), so the offset is the largest own - row
-            rel = torch.where(own >= 0, own - ar_q[None], -1 - sk)
+            # holes), none (left padding) or -- transformers / torch "unmask" rows that attend nothing --
+            # every key. The offset is the largest own - row over the rows that attend some key but not
+            # all of them; when no row qualifies (every row attends every key) the last query row is
+            # the last key's.
+            full = a.all(2)
+            rel = torch.where((own >= 0) & ~full, own - ar_q[None], -1 - sk)
             off = rel.amax(1)
-            q_valid = (own >= 0) & (rel == off[:, None])
+            off = torch.where(off < -sk, torch.full_like(off, sk - sq), off)
+            q_valid = (own >= 0) & (own - ar_q[None] == off[:, None])
             qpos = off[:, None] + ar_q[None]  # [B, Sq]
         else:  # (a decode row, Sq == 1, no query range: computed whatever its position; real iff it
             # attends a key)
@@ -170,6 +176,12 @@ def lower_mask(attention_mask: Optional[torch.Tensor], sq: int, sk: int, causal:
         allowed = kv_valid[:, None, :] & shape
         # (rows that do not attend their own key are padding: their output is discarded)
         shape_ok = ~((a != allowed) & q_valid[:, :, None]).any(2).any(1)
+        if causal:
+            # ... and a padding row's own position holds a padding key: a row left out whose own key a
+            # real row attends would be a real row the lowering drops (its output would be 0)
+            inside = (qpos >= 0) & (qpos < sk)
+            own_real = kv_valid.gather(1, qpos.clamp(0, sk - 1)) & inside
+            shape_ok = shape_ok & ~(own_real & ~q_valid).any(1)
     else:
         raise NotImplementedError(f"flash_attention_cute_amd: attention_mask with {m.dim()} dims")
     k_first, k_last, k_cnt = _first_last_count(kv_valid)
@@ -271,6 +283,37 @@ def _capturing(t: torch.Tensor) -> bool:
     return t.is_cuda and torch.cuda.is_current_stream_capturing()
 
 
+# The eager lowering of the last mask seen: (weak reference to the mask, its key, (lowering, path)). The
+# decoder layers of one forward receive the SAME mask tensor, so the device lowering and its one host
+# read run once per forward (per decode token), not once per layer. A hit needs the same live tensor
+# object (a weak reference: a freed mask whose id or storage is reused never matches) at the same
+# version counter (an in-place update misses). Never consulted under graph capture, whose lowering must
+# be recorded in the graph itself.
+_LOWER_MEMO: list = [None]
+
+
+def _lowered_eager(attention_mask: Optional[torch.Tensor], sq: int, sk: int, causal: bool,
+                   window_left: Optional[int]):
+    """``lower_mask`` + the path it allows (one host read), memoised across the layers of one forward:
+    (None, "dense") without a mask, else (lowering, "dense" | "padded" | "varlen")."""
+    if attention_mask is None:
+        return None, "dense"
+    key = (tuple(attention_mask.shape), attention_mask.dtype, attention_mask.device, attention_mask._version, sq, sk,
+           causal, window_left, TRUST_PADDING_MASK)
+    memo = _LOWER_MEMO[0]
+    if memo is not None and memo[0]() is attention_mask and memo[1] == key:
+        return memo[2]
+    low = lower_mask(attention_mask, sq, sk, causal, window_left)
+    if TRUST_PADDING_MASK:
+        path = "padded"
+    else:
+        shape_ok, run_ok, dense = torch.stack([low.shape_ok.all(), low.run_ok.all(), low.dense]).tolist()
+        _raise_unexpressible(shape_ok, run_ok, window_left)
+        path = "dense" if dense else "padded" if run_ok else "varlen"
+    _LOWER_MEMO[0] = (weakref.ref(attention_mask), key, (low, path))
+    return low, path
+
+
 def _flash_attention_forward(module: nn.Module, query: torch.Tensor, key: torch.Tensor, value: torch.Tensor,
                              attention_mask: Optional[torch.Tensor], dropout: float = 0.0,
                              scaling: Optional[float] = None, sliding_window: Optional[int] = None,
@@ -295,24 +338,23 @@ def _flash_attention_forward(module: nn.Module, query: torch.Tensor, key: torch.
     wl = -1 if window_left is None else window_left
     rope = kwargs.pop("rope_q", None)  # (cos, sin): q still to be rotated (fused path)
     kwargs.pop("cache_position", None)
-    low = lower_mask(attention_mask, sq, sk, causal, window_left)
-    if low is not None:
-        ranges = (low.k_start, low.k_end, low.q_start, low.q_end)
+    if attention_mask is not None and _capturing(query):
+        low = lower_mask(attention_mask, sq, sk, causal, window_left)
         path = "padded"
-        if TRUST_PADDING_MASK:
-            pass
-        elif _capturing(query):
+        ranges = (low.k_start, low.k_end, low.q_start, low.q_end)
+        if not TRUST_PADDING_MASK:
             # no host read-back: rows the padded kernel cannot express get empty ranges and are counted
             ok = low.shape_ok & low.run_ok
             _error_counter(query.device).add_((~ok).sum(dtype=torch.int32))
             ranges = (low.k_start, torch.where(ok, low.k_end, low.k_start), low.q_start,
                       torch.where(ok, low.q_end, low.q_start))
-        else:
+    else:
+        low, path = _lowered_eager(attention_mask, sq, sk, causal, window_left)
+        if low is not None:
+            ranges = (low.k_start, low.k_end, low.q_start, low.q_end)
             if query.is_cuda:
                 _error_counter(query.device)
-            shape_ok, run_ok, dense = torch.stack([low.shape_ok.all(), low.run_ok.all(), low.dense]).tolist()
-            _raise_unexpressible(shape_ok, run_ok, window_left)
-            path = "dense" if dense else "padded" if run_ok else "varlen"
+    if low is not None:
         if path != "dense":
             if rope is not None:
                 query = apply_rope(query, *rope)

@@ -43,7 +43,10 @@
 extern "C" {
 #endif
 
-#define FA_GFX950_ABI_VERSION 6
+/* 7: fa_fwd_gfx950_ws takes the key-split layout only when the workspace is large enough (a smaller one
+ *    runs the zigzag layout instead of failing), its counters live in a per-(device, stream) area the
+ *    library keeps zeroed (no per-call memset), and fa_split_errors() reports failed hand-offs. */
+#define FA_GFX950_ABI_VERSION 7
 
 /* Field order mirrors reference csrc/flash_attention.h:5-37. */
 typedef struct fa_fwd_params {
@@ -108,11 +111,16 @@ int fa_fwd_gfx950(const fa_fwd_params *params, int dtype, int causal, void *stre
  * persistent grid (at most one block per CU: a single long sequence, one GPU's
  * share of a multi-GPU split) with at least 3072 keys (2048 when the blocks fill
  * at most half the CUs) splits each block's keys in two pieces on two
- * workgroups instead; the workspace then holds the first piece's fp32 partial O
- * and the per-block counters (zeroed by this call on `stream` before the launch).
- * With workspace == NULL it behaves exactly like fa_fwd_gfx950 (decode kernel
- * unsplit, causal prefill in zigzag blocks). The workspace is scratch: it may be
- * reused as soon as the launch completes in stream order. 16-byte aligned.
+ * workgroups instead, when the workspace holds at least
+ * fa_fwd_gfx950_workspace_size() bytes (else the blocks run unsplit, in zigzag
+ * order); the workspace then holds the first piece's fp32 partial O. The pieces'
+ * per-block counters live in a device area the library allocates once per
+ * (device, stream) outside graph capture and the kernel leaves zeroed (under
+ * capture with no area yet, the counters go to the workspace, zeroed by this
+ * call on `stream`). With workspace == NULL it behaves exactly like
+ * fa_fwd_gfx950 (decode kernel unsplit, causal prefill in zigzag blocks). The
+ * workspace is scratch: it may be reused as soon as the launch completes in
+ * stream order. 16-byte aligned.
  * No reference counterpart (split-KV is a TODO at reference README.md:20).
  */
 int fa_fwd_gfx950_ws(const fa_fwd_params *params, int dtype, int causal, void *workspace,
@@ -130,6 +138,14 @@ int64_t fa_fwd_gfx950_workspace_size(const fa_fwd_params *params, int dtype, int
  * device. Returns FA_OK or the error code fa_fwd_gfx950 would return.
  */
 int fa_fwd_gfx950_check(const fa_fwd_params *params, int dtype, int causal);
+
+/*
+ * Key-split hand-offs on the current device that timed out (a piece whose partner's
+ * partial result did not arrive within ~1 s combined what was there: its rows are
+ * wrong), summed over launches since the last reset; 0 when none. Synchronises
+ * with the device. reset != 0 zeroes the count.
+ */
+int64_t fa_split_errors(int reset);
 
 /* Message for the last non-OK return on this thread ("" if none). */
 const char *fa_last_error(void);

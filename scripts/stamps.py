@@ -52,7 +52,8 @@ p = P(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), cfg["B"], cfg["Hq"
       *[t.stride(0) for t in st], *[t.stride(1) for t in st], *[t.stride(2) for t in st],
       cfg["D"] ** -0.5 * 1.4426950408889634)
 nwg = cfg["B"] * cfg["Hq"] * ((cfg["Sq"] + 255) // 256)
-W = int(os.environ.get("STAMPS_WIDTH", "12"))  # 16: a -DFA_STAMPS_FINE build (phase sub-splits)
+W = int(os.environ.get("STAMPS_WIDTH", "13"))  # 17: a -DFA_STAMPS_FINE build (phase sub-splits); 12 / 16: builds
+# before round 5 (no first-tile field)
 buf = torch.zeros(nwg * WAVES * W, dtype=torch.int64, device=dev)
 stream = torch.cuda.current_stream().cuda_stream
 lib.fa_debug_set_stamps(ctypes.c_void_p(0))
@@ -84,7 +85,7 @@ for i, nm in enumerate(names):
 tiles = s[:, 5].clamp(min=1)
 for i, nm in [(1, "p1"), (2, "p2+resc"), (3, "dma_wait"), (4, "barrier")]:
     print(f"  per tile {nm:10s} {float((s[:, i] / tiles).median()):8.0f} cycles")
-if W == 16:  # FA_STAMPS_FINE: phase 2 in quarters (8 of its 32 MFMA gaps each), phase 1 in halves
+if W in (16, 17):  # FA_STAMPS_FINE: phase 2 in quarters (8 of its 32 MFMA gaps each), phase 1 in halves
     q = [float((s[:, i] / tiles).median()) for i in (12, 13, 14)]
     p2t = float((s[:, 2] / tiles).median())
     h1 = float((s[:, 15] / tiles).median())
@@ -121,7 +122,8 @@ bt = torch.quantile(w0[:, 0], torch.tensor([0.1, 0.5, 0.9, 1.0], dtype=torch.flo
 btl = torch.quantile(w0[:, 5], torch.tensor([0.1, 0.5, 0.9, 1.0], dtype=torch.float64))
 print(f"  block cycles (wave 0) p10 {bt[0]:.0f}  p50 {bt[1]:.0f}  p90 {bt[2]:.0f}  max {bt[3]:.0f}; "
       f"tiles p10 {btl[0]:.0f}  p50 {btl[1]:.0f}  p90 {btl[2]:.0f}  max {btl[3]:.0f}")
-for i, nm in [(6, "drain"), (7, "prologue"), (8, "epilogue")]:
+fields = [(6, "drain"), (7, "prologue"), (8, "epilogue")] + ([(W - 1, "first tile")] if W in (13, 17) else [])
+for i, nm in fields:
     qs = torch.quantile(s[:, i], torch.tensor([0.1, 0.5, 0.9, 0.99], dtype=torch.float64))
     print(f"  {nm:10s} p10 {qs[0]:8.0f}  p50 {qs[1]:8.0f}  p90 {qs[2]:8.0f}  p99 {qs[3]:8.0f}")
 if WAVES == 8:  # leaders (waves 0-3) and followers (4-7) of every block

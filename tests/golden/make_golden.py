@@ -21,10 +21,13 @@ inputs and stores inputs + outputs as fixtures:
                      csrc/flash_attention_template.cuh:157-160); the UNEXPANDED inputs are stored.
                      Sq == 1 cases are the GPU's q-head pack (reference
                      csrc/flash_attention_api.cpp:72-83) with g = 4 and g = 8.
+  golden_gqa128.npz  the same at D = 128 (see GQA128_SPEC): causal g = 4 in fp16 and bf16, the Sq == 1
+                     pack, and one long causal head that the default key-split rule runs in two pieces
   golden_meta.json   the op schema and the reference's error on a GQA call on CPU
 
 No bytecode is written into /root/reference. Re-run with:  python tests/golden/make_golden.py
-(``--multi`` / ``--gqa`` regenerate only golden_multi.npz / golden_gqa.npz).
+(``--multi`` / ``--gqa`` / ``--gqa128`` regenerate only golden_multi.npz / golden_gqa.npz /
+golden_gqa128.npz).
 """
 from __future__ import annotations
 
@@ -115,12 +118,22 @@ GQA_SPEC = [
     ("bf16", torch.bfloat16, 1, 32, 8, 1, 128, 64, False),   # decode pack at Llama-3-8B's Hq32 / Hkv8
 ]
 GQA_CODE_SCALE = 4.0
+# D = 128 cases (golden_gqa128.npz): the head dim C4 / C5 run on, and the default
+# key-split layout. Seeds 3000 + i.
+GQA128_SPEC = [
+    ("f16", torch.float16, 1, 4, 1, 512, 512, 128, True),    # C4's class: fp16 causal g = 4, 2 Q blocks
+    ("bf16", torch.bfloat16, 1, 4, 1, 640, 640, 128, True),  # C5's class: bf16 causal g = 4, ragged Q block
+    ("f16", torch.float16, 2, 8, 2, 1, 384, 128, False),     # decode pack at D = 128, g = 4
+    ("f16", torch.float16, 1, 1, 1, 2048, 2048, 128, True),  # one causal head of 2048: the default rule's
+                                                             # key-split layout (8 blocks <= half the CUs)
+]
 
 
-def make_gqa(ref) -> int:
+def make_gqa(ref, spec=None, fname="golden_gqa.npz", seed0=2000) -> int:
+    spec = GQA_SPEC if spec is None else spec
     cases = {}
-    for i, (name, dt, b, hq, hkv, sq, sk, d, causal) in enumerate(GQA_SPEC):
-        gen = torch.Generator().manual_seed(2000 + i)
+    for i, (name, dt, b, hq, hkv, sq, sk, d, causal) in enumerate(spec):
+        gen = torch.Generator().manual_seed(seed0 + i)
         codes = [torch.randint(-8, 8, (b, h, s, d), generator=gen, dtype=torch.int8)
                  for h, s in ((hq, sq), (hkv, sk), (hkv, sk))]
         q, k, v = (c.to(dt) / GQA_CODE_SCALE for c in codes)  # exact: |code| <= 8, power-of-two scale
@@ -135,12 +148,19 @@ def make_gqa(ref) -> int:
         cases[f"{key}_dtype"] = np.array(name)
         cases[f"{key}_scale"] = np.float64(d ** -0.5)
     cases["code_scale"] = np.float64(GQA_CODE_SCALE)
-    np.savez_compressed(OUT / "golden_gqa.npz", **cases)
-    return len(GQA_SPEC)
+    np.savez_compressed(OUT / fname, **cases)
+    return len(spec)
 
 
 def main() -> None:
     ref = import_reference_op()
+    if "--gqa128" in sys.argv:  # regenerate only golden_gqa128.npz (+ its count in golden_meta.json)
+        warnings.simplefilter("ignore")
+        meta = json.loads((OUT / "golden_meta.json").read_text())
+        meta["n_gqa128_cases"] = make_gqa(ref, GQA128_SPEC, "golden_gqa128.npz", 3000)
+        (OUT / "golden_meta.json").write_text(json.dumps(meta, indent=1) + "\n")
+        print(json.dumps(meta, indent=1))
+        return
     if "--gqa" in sys.argv:  # regenerate only golden_gqa.npz (+ its count in golden_meta.json)
         warnings.simplefilter("ignore")
         meta = json.loads((OUT / "golden_meta.json").read_text())
@@ -195,6 +215,7 @@ def main() -> None:
         gqa_err = str(e).splitlines()[0]
     meta = {"schema": schema, "cpu_gqa_error": gqa_err, "n_small_cases": len(spec), "n_multi_cases": make_multi(ref),
             "n_gqa_cases": make_gqa(ref),
+            "n_gqa128_cases": make_gqa(ref, GQA128_SPEC, "golden_gqa128.npz", 3000),
             "generator": "reference flash_attention/flash_attention.py CPU path, torch " + torch.__version__}
     (OUT / "golden_meta.json").write_text(json.dumps(meta, indent=1) + "\n")
     print(json.dumps(meta, indent=1))

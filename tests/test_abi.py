@@ -44,7 +44,7 @@ def test_header_declares_the_boundary():
                                          "fa_fwd_gfx950_workspace_size", "fa_fwd_gfx950_varlen",
                                          "fa_fwd_gfx950_varlen_check", "fa_fwd_gfx950_rope", "fa_rope_gfx950",
                                          "fa_fwd_gfx950_window", "fa_fwd_gfx950_varlen_window", "fa_fwd_gfx950_padded",
-                                         "fa_fwd_gfx950_padded_workspace_size"}
+                                         "fa_fwd_gfx950_padded_workspace_size", "fa_split_errors"}
 
 
 def test_every_declared_symbol_is_exported(lib):
@@ -84,7 +84,7 @@ def check(lib, p, dtype=0, causal=0):
 
 def test_abi_version(lib):
     lib.fa_abi_version.restype = ctypes.c_int
-    assert lib.fa_abi_version() == 6
+    assert lib.fa_abi_version() == 7
 
 
 def test_check_accepts_valid(lib):

@@ -126,6 +126,41 @@ def test_reference_golden_gqa_vectors_on_gpu(op, device):
     assert all(p == "w4" for (sq, _), p in paths.items() if sq > 1), paths
 
 
+def test_reference_golden_gqa128_vectors_on_gpu(op, device):
+    """D = 128 pinned to the REFERENCE's outputs (golden_gqa128.npz): causal
+    g = 4 in fp16 and bf16 -- the head dim and q-head mapping C4 / C5 run -- the Sq == 1 pack at D = 128
+    on the decode kernel, and one causal head of 2048 keys that the DEFAULT key-split rule runs as two
+    pieces per block (the layout C4's 8-way share takes)."""
+    import flash_attention_cute_amd as m
+    from flash_attention_cute_amd import _debug
+
+    g = np.load(GOLD / "golden_gqa128.npz")
+    n = json.loads((GOLD / "golden_meta.json").read_text())["n_gqa128_cases"]
+    assert n == 4
+    cs = float(g["code_scale"])
+    _debug.set_knobs()
+    _debug.set_split()  # (the default rule)
+    m.split_errors(reset=True)
+    layouts = {}
+    for i in range(n):
+        dtype = str(g[f"case{i}_dtype"])
+        b, hq, hkv, sq, sk, d, causal = (int(x) for x in g[f"case{i}_meta"])
+        assert d == 128
+        tdt = torch.float16 if dtype == "f16" else torch.bfloat16
+        q, k, v = (torch.from_numpy(g[f"case{i}_{n_}c"]).to(tdt).div_(cs).to(device) for n_ in "qkv")
+        ref = _gold_tensor(g[f"case{i}_o"], dtype).float()
+        out = op(q, k, v, causal=bool(causal)).float().cpu()
+        layouts[i] = (_debug.last_path(), _debug.last_layout() if sq > 1 else None)
+        tol = {"f16": 2e-3, "bf16": 1.6e-2}[dtype]
+        err = (out - ref).abs()
+        assert (err <= tol + tol * ref.abs()).all(), (i, err.max().item())
+        assert err.mean().item() < tol / 8, (i, err.mean().item())
+    assert layouts[2][0].startswith("decode"), layouts
+    assert layouts[3] == ("w4", "split"), layouts  # B1 Hq1 S2048 causal: key-split by default
+    assert all(p == "w4" for p, _ in (layouts[0], layouts[1])), layouts
+    assert m.split_errors() == 0
+
+
 @pytest.mark.parametrize("causal", [False, True])
 def test_reference_module_path_pybind_call_matches_flash_attn_func(op, device, causal):
     """Code written against the reference's submodule: ``flash_attention.flash_attention

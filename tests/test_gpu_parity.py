@@ -381,6 +381,7 @@ def test_key_split_causal_blocks(device, shape, dtype):
     qd, kd, vd = q.to(device), k.to(device), v.to(device)
     _debug.set_knobs()
     _debug.set_split(2)
+    m.split_errors(reset=True)
     try:
         out = m.flash_attn_func(qd, kd, vd, causal=True)
         assert _debug.last_path() == "w4" and _debug.last_layout() == "split"
@@ -396,6 +397,9 @@ def test_key_split_causal_blocks(device, shape, dtype):
     finally:
         _debug.set_split()
         _debug.set_zigzag()
+    # (the counters of the persistent per-stream area were left zeroed by every launch: a stale one
+    # would have sent the next launch's pieces to the wrong records)
+    assert m.split_errors() == 0
     assert torch.equal(out, again) and torch.equal(out, small)
     check(out, q, k, v, d ** -0.5, True, dtype)
     tol = 4e-3 if dtype == torch.float16 else 3e-2
@@ -429,10 +433,16 @@ def test_key_split_only_with_a_workspace(device):
         p.o_ptr = o2.data_ptr()
         lib.fa_fwd_gfx950_ws.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
                                          ctypes.c_void_p]
-        assert lib.fa_fwd_gfx950_ws(ctypes.byref(p), 0, 1, ws.data_ptr(), need - 256, stream) == 1  # too small
+        o3 = torch.empty_like(q)
+        p.o_ptr = o3.data_ptr()
+        # (ABI 7: a workspace too small for the partials runs the unsplit zigzag layout, no error)
+        assert lib.fa_fwd_gfx950_ws(ctypes.byref(p), 0, 1, ws.data_ptr(), need - 256, stream) == 0
+        assert _debug.last_layout() == "zigzag"
+        p.o_ptr = o2.data_ptr()
         assert lib.fa_fwd_gfx950_ws(ctypes.byref(p), 0, 1, ws.data_ptr(), need, stream) == 0
         assert _debug.last_layout() == "split"
         torch.cuda.synchronize()
+        assert torch.equal(o, o3)
         assert (o.float() - o2.float()).abs().max().item() < 4e-3
         # default knob: 8 x 32 heads x 4 q-tiles = 1024 blocks, four rounds, and this one-round 1024-key
         # launch ask for none; 8 heads x 16 q-tiles of 4096 keys (128 blocks) does (contiguous strides)
@@ -448,3 +458,30 @@ def test_key_split_only_with_a_workspace(device):
         assert lib.fa_fwd_gfx950_workspace_size(ctypes.byref(params(1, 8, 2, 4096)), 0, 1) > 0
     finally:
         _debug.set_split()
+
+
+def test_key_split_under_graph_capture(device):
+    """A key-split launch captured into a HIP graph: the capturing stream has no counter area yet, so its
+    counters go to the workspace, zeroed by a memset node of the graph; replays equal the eager launch
+    bit for bit, and no hand-off times out."""
+    import flash_attention_cute_amd as m
+    from flash_attention_cute_amd import _debug
+
+    q, k, v = (t.to(device) for t in make(1, 4, 2, 1024, 1024, 128, torch.bfloat16, 21))
+    _debug.set_split(2)
+    m.split_errors(reset=True)
+    try:
+        eager = m.flash_attn_func(q, k, v, causal=True)
+        assert _debug.last_layout() == "split"
+        g = torch.cuda.CUDAGraph()  # (captures on a stream of its own)
+        with torch.cuda.graph(g):
+            out = m.flash_attn_func(q, k, v, causal=True)
+        outs = []
+        for _ in range(3):
+            g.replay()
+            outs.append(out.clone())
+        torch.cuda.synchronize()
+    finally:
+        _debug.set_split()
+    assert all(torch.equal(o, eager) for o in outs)
+    assert m.split_errors() == 0

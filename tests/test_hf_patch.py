@@ -9,6 +9,7 @@ transformers (SDPA) on the same device.
 from __future__ import annotations
 
 import copy
+import sys
 import warnings
 
 import pytest
@@ -446,6 +447,67 @@ def test_lower_mask_static_cache_and_padding_kinds():
     doc = _static_masks(torch.ones(1, total, dtype=torch.bool), 0, 7, total)[:, :, :7].clone()
     doc[0, 0, 4:, :4] = False
     assert lower_mask(doc, 7, total, True).shape_ok.tolist() == [False]
+
+
+def test_lower_mask_unmasked_left_padding_rows():
+    """transformers / torch "unmask" query rows that attend nothing (left padding) to attend EVERY key.
+    Such a row must not set the causal offset (it made the padding row the only valid
+    query and zeroed the real rows); a real row left out of the query range is rejected, not zeroed."""
+    from flash_attention_cute_amd.hf_attention import lower_mask
+
+    sq = sk = 8
+    valid = torch.zeros(2, sk, dtype=torch.bool)
+    valid[0, 3:] = True  # three left-padding tokens
+    valid[1, :] = True
+    m = _static_masks(valid, 0, sq, sk).clone()  # [B, 1, Sq, Sk], dynamic-cache prefill
+    m[0, 0, :3, :] = True  # the padding rows unmasked
+    low = lower_mask(m, sq, sk, True)
+    assert low.q_start.tolist() == [3, 0] and low.q_end.tolist() == [8, 8]
+    assert low.k_start.tolist() == [3, 0] and low.k_end.tolist() == [8, 8]
+    assert low.shape_ok.tolist() == [True, True] and low.run_ok.tolist() == [True, True]
+    # the additive float form of the same mask
+    lowf = lower_mask(torch.where(m, 0.0, float("-inf")), sq, sk, True)
+    assert lowf.q_start.tolist() == [3, 0] and lowf.shape_ok.tolist() == [True, True]
+    # every row unmasked (a sequence of padding only, but its last token): only the last row is real
+    m2 = torch.ones(1, 1, sq, sk, dtype=torch.bool)
+    low2 = lower_mask(m2, sq, sk, True)
+    assert low2.q_start.tolist() == [7] and low2.q_end.tolist() == [8]
+    # a real row that hides its own key (not causal + padding) is rejected instead of being dropped
+    m3 = _static_masks(torch.ones(1, sk, dtype=torch.bool), 0, sq, sk).clone()
+    m3[0, 0, 5, 5] = False
+    assert lower_mask(m3, sq, sk, True).shape_ok.tolist() == [False]
+
+
+def test_eager_padded_forward_reads_the_host_once_per_forward(monkeypatch):
+    """the layers of one forward share the lowering of their (identical) mask,
+    so an eager left-padded forward through a 4-layer model does ONE host read, not one per layer; a new
+    mask (or an in-place change) is lowered again."""
+    cfg = tiny_llama(hq=4, hkv=2, d=32, layers=4)
+    torch.manual_seed(0)
+    model = transformers.LlamaForCausalLM(cfg).eval()
+    ids = torch.randint(1, cfg.vocab_size, (2, 9))
+    mask = torch.ones_like(ids)
+    mask[1, :4] = 0
+    reads = []  # host reads made by the attention patch (transformers' own code makes others)
+    orig = torch.Tensor.tolist
+
+    def counted(self):
+        if sys._getframe(1).f_code.co_filename.endswith("hf_attention.py"):
+            reads.append(1)
+        return orig(self)
+
+    monkeypatch.setattr(torch.Tensor, "tolist", counted)
+    lowers = []
+    monkeypatch.setattr(hf_attention, "lower_mask", lambda *a, _f=hf_attention.lower_mask: (lowers.append(1), _f(*a))[1])
+    hf_attention._LOWER_MEMO[0] = None
+    with torch.no_grad(), warnings.catch_warnings(), patched(ml.LlamaAttention):
+        warnings.simplefilter("ignore")
+        out = model(ids, attention_mask=mask).logits
+        assert len(reads) == 1 and len(lowers) == 1
+        model(ids, attention_mask=mask)
+        assert len(reads) == 2 and len(lowers) == 2  # (a new forward builds a new mask tensor)
+    ref = model(ids, attention_mask=mask).logits
+    assert torch.allclose(out[1, 4:], ref[1, 4:], atol=1e-4, rtol=1e-4) and torch.allclose(out[0], ref[0], atol=1e-4)
 
 
 class _NoHostReads:

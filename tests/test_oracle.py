@@ -188,6 +188,19 @@ def test_golden_gqa_cases(i):
     assert np.abs(out - o).mean() < atol / 8
 
 
+@pytest.mark.parametrize("i", range(json.loads((GOLD / "golden_meta.json").read_text())["n_gqa128_cases"]))
+def test_golden_gqa128_cases(i):
+    """The same at D = 128 (golden_gqa128.npz): causal g = 4 in fp16 (C4's class)
+    and bf16 (C5's), the Sq == 1 pack at D = 128, one long causal head (the GPU's key-split layout)."""
+    g = np.load(GOLD / "golden_gqa128.npz")
+    q, k, v, o, dtype, scale, causal, _ = load_gqa_case(g, i)
+    assert q.shape[-1] == 128
+    out = O.flash_attention_fwd(q, k, v, scale, causal, dtype)
+    atol = {"f16": 2e-3, "bf16": 1.6e-2}[dtype]
+    np.testing.assert_allclose(out, o, atol=atol, rtol=atol)
+    assert np.abs(out - o).mean() < atol / 8
+
+
 def test_golden_gqa_covers_the_pack_and_the_mapping():
     g = np.load(GOLD / "golden_gqa.npz")
     n = json.loads((GOLD / "golden_meta.json").read_text())["n_gqa_cases"]
