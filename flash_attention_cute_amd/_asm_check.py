@@ -98,6 +98,8 @@ _BRANCH = re.compile(r"^s_(cbranch_\w+|branch)$")
 _STORE = re.compile(r"^(ds_write|ds_store|buffer_store|global_store|flat_store|scratch_store)")
 _LOAD = re.compile(r"^(ds_read|ds_load|buffer_load|global_load|flat_load|scratch_load)")
 HORIZON = 40  # wait states after which no rule applies any more
+MAX_CTX = 8  # path contexts (branch-flag values) kept per basic block
+MAX_FLAGS = 4  # branch flags tracked at once
 
 
 def _regs(op: str):
@@ -215,6 +217,43 @@ def _classify(mn, ops):
     return "other", [], [], [], [], []
 
 
+_SREG = re.compile(r"^s\[(\d+):(\d+)\]$|^s(\d+)$")
+
+
+def _sregs(op: str):
+    m = _SREG.match(op)
+    if not m:
+        return None
+    return (int(m.group(1)), int(m.group(2))) if m.group(1) else (int(m.group(3)), int(m.group(3)))
+
+
+def _flow_const(kc: dict, vcc, mn: str, ops: list):
+    """Branch-flag constants (the walk prunes the infeasible edges of hipcc's structurised control flow):
+    hipcc sets an SGPR pair to -1 / 0 on each incoming edge of a join and tests it after the join
+    (``s_mov_b64 s[x:y], -1`` ... ``s_and_b64 vcc, exec, s[x:y]`` / ``s_cbranch_vccz``). kc maps a pair to
+    its known value; vcc is "nz" / "z" / None. Returns the new vcc; kc is updated in place. Conservative:
+    any other instruction naming vcc makes it unknown, and any SGPR a VALU instruction names or an SALU
+    instruction writes (its first operand) drops the pairs it overlaps."""
+    if mn in ("s_and_b64", "s_andn2_b64") and len(ops) == 3 and ops[0] == "vcc" and ops[1] == "exec":
+        # (a flag is tested once after its join: it is forgotten here, which keeps the contexts few)
+        v = kc.pop(_sregs(ops[2]), None)
+        if v is None:
+            return None
+        nz = (v != 0) if mn == "s_and_b64" else (v == 0)  # (exec is not empty inside the kernel)
+        return "nz" if nz else "z"
+    if any(o.startswith("vcc") for o in ops):
+        vcc = None
+    named = [r for r in (_sregs(o) for o in (ops if mn.startswith("v_") else ops[:1])) if r is not None]
+    for dst in named:
+        for k in [k for k in kc if not (k[1] < dst[0] or k[0] > dst[1])]:
+            del kc[k]
+    if mn == "s_mov_b64" and len(ops) == 2 and ops[1] in ("-1", "0") and named and named[0][1] == named[0][0] + 1:
+        kc[named[0]] = int(ops[1])
+        while len(kc) > MAX_FLAGS:  # (the most recently set flags only)
+            del kc[next(iter(kc))]
+    return vcc
+
+
 def hazards(text: str) -> list[str]:
     """Violations of R1-R4 around the inline-asm MFMAs of every fa_fwd_w4 kernel in ``text``."""
     out = []
@@ -224,14 +263,20 @@ def hazards(text: str) -> list[str]:
             continue
         # state: valu[reg] = slots since its last VALU write; mf[reg] = (slots since an asm MFMA wrote
         # it, required); pipe = slots until the MFMA pipe is free
-        entry = [None] * len(blocks)
-        entry[0] = ({}, {}, 0, frozenset(("a", r) for r in range(256)))
-        work = [0]
+        # Path contexts: a block keeps one state per (known branch flags, vcc) combination it is entered
+        # with (at most MAX_CTX, then they are merged into the flag-free context), so a state that
+        # reaches a join only on the edge whose flag value skips a branch is not paired with it
+        entry = [dict() for _ in blocks]
+        entry[0][((), None)] = ({}, {}, 0, frozenset(("a", r) for r in range(256)))
+        work = [(0, ((), None))]
         seen_err = set()
         while work:
-            bi = work.pop()
-            valu, mf, pipe = (dict(entry[bi][0]), dict(entry[bi][1]), entry[bi][2])
-            stale = set(entry[bi][3])
+            bi, key = work.pop()
+            if key not in entry[bi]:
+                continue
+            valu, mf, pipe = (dict(entry[bi][key][0]), dict(entry[bi][key][1]), entry[bi][key][2])
+            stale = set(entry[bi][key][3])
+            kc, vcc = dict(key[0]), key[1]
 
             def advance(n):
                 nonlocal pipe
@@ -249,6 +294,7 @@ def hazards(text: str) -> list[str]:
                 pipe = max(0, pipe - n)
 
             for _, mn, ops, in_asm, ln in blocks[bi][1]:
+                vcc = _flow_const(kc, vcc, mn, ops)
                 kind, dst, sa, sb, sc, srcs = _classify(mn, ops)
                 if kind == "mfma":
                     advance(pipe)  # stall until the pipe accepts it
@@ -296,12 +342,35 @@ def hazards(text: str) -> list[str]:
                         valu[reg] = 0
                     else:
                         valu.pop(reg, None)
-            for s in succ[bi]:
-                if entry[s] is None:
-                    entry[s] = ({k: v for k, v in valu.items()}, dict(mf), pipe, frozenset(stale))
-                    work.append(s)
+            body = blocks[bi][1]
+            nxt = list(succ[bi])
+            if body and body[-1][1] in ("s_cbranch_vccz", "s_cbranch_vccnz") and vcc is not None and len(nxt) == 2:
+                taken = (vcc == "z") == (body[-1][1] == "s_cbranch_vccz")
+                nxt = [nxt[0]] if taken else [nxt[1]]  # (succ: [branch target, fall-through])
+            for s in nxt:
+                nkey = (tuple(sorted(kc.items())), vcc)
+                if nkey not in entry[s] and len(entry[s]) >= MAX_CTX:
+                    nkey = ((), None)
+                    if nkey not in entry[s]:  # merge every context into the flag-free one
+                        for k in list(entry[s]):
+                            st = entry[s].pop(k)
+                            if nkey not in entry[s]:
+                                entry[s][nkey] = st
+                                continue
+                            a, b_ = entry[s][nkey], st
+                            mv = dict(a[0])
+                            for kk, vv in b_[0].items():
+                                mv[kk] = min(vv, mv.get(kk, HORIZON + 1))
+                            mm = dict(a[1])
+                            for kk, (t, req) in b_[1].items():
+                                if kk not in mm or t < mm[kk][0]:
+                                    mm[kk] = (t, max(req, mm.get(kk, (0, 0))[1]))
+                            entry[s][nkey] = (mv, mm, min(a[2], b_[2]), a[3] | b_[3])
+                if nkey not in entry[s]:
+                    entry[s][nkey] = ({k: v for k, v in valu.items()}, dict(mf), pipe, frozenset(stale))
+                    work.append((s, nkey))
                     continue
-                ov, om, op_, ost = entry[s]
+                ov, om, op_, ost = entry[s][nkey]
                 nv = dict(ov)
                 for k, v in valu.items():
                     nv[k] = min(v, nv.get(k, HORIZON + 1))
@@ -312,8 +381,8 @@ def hazards(text: str) -> list[str]:
                 npipe = min(op_, pipe)  # (the smaller stall: elapsed time is a lower bound)
                 nst = ost | frozenset(stale)
                 if (nv, nm, npipe, nst) != (ov, om, op_, ost):
-                    entry[s] = (nv, nm, npipe, nst)
-                    work.append(s)
+                    entry[s][nkey] = (nv, nm, npipe, nst)
+                    work.append((s, nkey))
         out += sorted(seen_err)
     return out
 

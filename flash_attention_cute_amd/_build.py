@@ -77,6 +77,13 @@ def _jobs() -> int:
     return max(1, min(int(n), 16))
 
 
+def _process_pool():
+    """Worker processes for the assembly gate (a pure-Python dataflow over each instantiation, seconds each)."""
+    from concurrent.futures import ProcessPoolExecutor
+
+    return ProcessPoolExecutor(max_workers=_jobs())
+
+
 def build_abi(force: bool = False, verbose: bool = False, stamps: bool = False, tag: str = "",
               defines: tuple = (), flags: tuple = (), only: tuple = (), debug: bool = False,
               gate: bool = True) -> Path:
@@ -129,7 +136,8 @@ def build_abi(force: bool = False, verbose: bool = False, stamps: bool = False, 
     # gate: the literal-AGPR invariant of fa_fwd_w4 and no VGPR spills (_asm_check)
     from ._asm_check import check_file
 
-    problems = [p for a in asm_files for p in check_file(a)]
+    with ThreadPoolExecutor(max_workers=1) if len(asm_files) < 2 else _process_pool() as ex:
+        problems = [p for ps in ex.map(check_file, asm_files) for p in ps]
     if diag:  # stamp / experiment builds: spills are reported, not fatal (the AGPR rule stays)
         for q in [q for q in problems if "vgpr_spill_count" in q or not gate]:
             print(f"warning ({sdir}): {q}", flush=True)

@@ -212,7 +212,7 @@ int64_t fa::w4_grid(int64_t nwg) {
     return nwg < cap ? nwg : cap;
 }
 
-// Diagnostic hook (not in include/fa_gfx950.h): device buffer of 13 u64 per wave (17 with FA_STAMPS_FINE) of the next
+// Diagnostic hook (not in include/fa_gfx950.h): device buffer of 15 u64 per wave (19 with FA_STAMPS_FINE) of the next
 // launches; honoured only by a -DFA_STAMPS=1 build of the kernels (scripts/stamps.py).
 extern "C" void fa_debug_set_stamps(void *device_buffer) { g_stamps = (unsigned long long *)device_buffer; }
 

@@ -631,6 +631,14 @@ __device__ __forceinline__ void agpr_scale(const float alpha) {
     }
 }
 template <int BASE>
+__device__ __forceinline__ void agpr_read8(float *x) {
+#define FA_CASE(N) \
+    if constexpr (BASE == N) fa_agpr_read8_##N(x);
+    FA_CASE(0) FA_CASE(8) FA_CASE(16) FA_CASE(24) FA_CASE(32) FA_CASE(40) FA_CASE(48) FA_CASE(56)
+    FA_CASE(64) FA_CASE(72) FA_CASE(80) FA_CASE(88) FA_CASE(96) FA_CASE(104) FA_CASE(112) FA_CASE(120)
+#undef FA_CASE
+}
+template <int BASE>
 __device__ __forceinline__ f32x16 agpr_read16() {
     float x[16];
     if constexpr (BASE == 0) fa_agpr_read16_0(x);
@@ -642,7 +650,9 @@ __device__ __forceinline__ f32x16 agpr_read16() {
     else if constexpr (BASE == 96) fa_agpr_read16_96(x);
     else if constexpr (BASE == 112) fa_agpr_read16_112(x);
     else if constexpr (BASE == 128) fa_agpr_read16_128(x);
-    else fa_agpr_read16_144(x);
+    else if constexpr (BASE == 144) fa_agpr_read16_144(x);
+    else if constexpr (BASE == 160) fa_agpr_read16_160(x);
+    else fa_agpr_read16_176(x);
     f32x16 v;
 #pragma unroll
     for (int i = 0; i < 16; ++i) v[i] = x[i];
@@ -893,9 +903,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #define FA_STAMP(v) const uint32_t v = (uint32_t)__builtin_amdgcn_s_memtime()
 #ifdef FA_STAMPS_FINE  // (finer split: phase 2 at the ends of its quarters, phase 1 at its middle)
     uint32_t st_f[4] = {0, 0, 0, 0}, st_fa[4] = {0, 0, 0, 0};
-#define FA_STAMP_W 17
+#define FA_STAMP_W 19
 #else
-#define FA_STAMP_W 13
+#define FA_STAMP_W 15
 #endif
 #else
     (void)stamps;
@@ -920,6 +930,18 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     constexpr int QB = 128;  // Q fragments: AGPRs a[QB + 4*(X*KS + ks)] (fa_agpr_asm.inc)
 #ifndef FA_QLDS
 #define FA_QLDS 1
+#endif
+#ifndef FA_ZERO_MFMA  // O zeroed by 2 * DTL MFMAs in the prologue (0: 32 * DTL v_accvgpr_write)
+#define FA_ZERO_MFMA 1
+#endif
+#ifndef FA_DRAIN_OVL  // the drain's late softmax in its P.V MFMA gaps (0: all of it before the P.V)
+#define FA_DRAIN_OVL 1
+#endif
+#ifndef FA_EPI_OVL  // a block's O stores in the MFMA gaps of the next block's first tile (0: at its end;
+#define FA_EPI_OVL 0   // 1 measured -0.3 % C4, -0.8 % C5, -2 % on C4's 8-way share: profiles/r5b_ab_*.log)
+#endif
+#ifndef FA_SPLIT_AGPR  // key-split combine: partner records into the Q AGPRs, a block per round trip
+#define FA_SPLIT_AGPR 1  // (0: one d-tile of both blocks per round trip, into VGPRs)
 #endif
     // Q staging (kQL): 0 = HBM -> AGPR loads issued under the previous block's drain; 1 = LDS-DMA
     // into a Q image (K's swizzle) under the drain, read into the AGPRs at the block prologue;
@@ -1354,6 +1376,40 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     };
 
     const uint32_t lds_base = lds_u32(lds) + wave * NP * 1024;  // this wave's pieces of slot 0
+    // O = 0 (FA_ZERO_MFMA: 2 * DTL MFMAs 0 * 0 + 0, one issue slot per 16 AGPRs, worked off by the matrix
+    // pipe beside the VALU that follows; the block's first P.V MFMA, tile jb's phase 2, is the first reader)
+    auto zero_o = [&]() __attribute__((always_inline)) {
+#if FA_ZERO_MFMA
+        u32x4 z = {0, 0, 0, 0};
+        asm volatile("" : "+v"(z));
+        if constexpr (DTL == 4) fa_agpr_zmfma_4(z); else fa_agpr_zmfma_2(z);
+#else
+        if constexpr (DTL == 4) fa_agpr_zero_4(); else fa_agpr_zero_2();
+#endif
+    };
+    // Deferred epilogue (FA_EPI_OVL): a dense block that another block follows leaves O in the AGPRs
+    // and its stores to the next block's first tile, whose phase-1 gaps are free of softmax work (no
+    // tile -1): unit u is one 16-B store per lane (block X, d-tile dt, row pair gp) -- 8 AGPR reads,
+    // O / l, packing and a half-wave swap, as store_block
+    bool epi_pending = false;
+    float epi_inv0 = 1.f, epi_inv1 = 1.f;
+    rsrc_t epi_orr = make_rsrc(nullptr, 0u);
+    int epi_rowb = 0;
+    auto epi_unit = [&](auto U) __attribute__((always_inline)) {
+        constexpr int u = decltype(U)::value;
+        constexpr int X = u / (2 * DTL), dt = (u % (2 * DTL)) / 2, gp = (u & 1) * 2;
+        float x[8];
+        agpr_read8<16 * DTL * X + 16 * dt + 4 * gp>(x);
+        const float inv = X ? epi_inv1 : epi_inv0;
+        const uint32_t a0 = DT::pack(x[0] * inv, x[1] * inv), a1 = DT::pack(x[2] * inv, x[3] * inv);
+        const uint32_t b0 = DT::pack(x[4] * inv, x[5] * inv), b1 = DT::pack(x[6] * inv, x[7] * inv);
+        const auto x0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+        const auto x1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+        const int d0 = dt * 32 + 8 * (gp + h);
+        const int orow = r * (int)p.o_seqlen_stride * 2 + (X ? epi_rowb : 0);
+        __builtin_amdgcn_raw_buffer_store_b128((u32x4){x0[0], x1[0], x0[1], x1[1]}, epi_orr,
+                                               (kExactD || d0 < D) ? orow + 2 * d0 : 0x7ffffff0, 0, 0);
+    };
     // ---- softmax split: of each block's 32 scores of a tile (index q = 16 * half + v), q < kV0 are
     // exponentiated in phase 2 right after the tile's rescale decision ("early", summed into t), the
     // rest in the next phase 1 ("late", summed into l).
@@ -1379,6 +1435,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         constexpr bool do_sm = decltype(SM2)::value, do_dma = decltype(DMA)::value;
         constexpr bool sdead = decltype(AD)::value & 1, pdead = decltype(AD)::value & 2;
         constexpr bool vpre = decltype(AD)::value & 4;
+        // bit 3: a block's first tile with the previous block's deferred O stores (FA_EPI_OVL): its K / V
+        // pieces go first (gaps 0 .. 2 NP - 1), so the tile's closing wait can leave the stores in flight
+        constexpr bool epi = decltype(AD)::value & 8;
         u32x4 kf[2][2];  // [buffer][key half]
 #pragma unroll
         for (int x = 0; x < 2; ++x) kf[0][x] = *(const u32x4 *)(K + x * 32 * RB + k_addr[0]);
@@ -1432,9 +1491,18 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                     va_pre[n >> 1][2 * (n & 1) + 1] = x[1];
                 });
             }
-            if constexpr (do_dma && i == 2) {
-                if constexpr (ks < NP) dma_q_at<pr * T, ks * 1024>(kq, lds_base, kvo[ks]);
-                else dma_q_at<(2 + c) * T, (ks - NP) * 1024>(vq, lds_base, vvo[ks - NP]);
+            if constexpr (do_dma && (epi ? g < 2 * NP : i == 2)) {
+                constexpr int n = epi ? g : ks;  // (piece)
+                if constexpr (n < NP) dma_q_at<pr * T, n * 1024>(kq, lds_base, kvo[n]);
+                else dma_q_at<(2 + c) * T, (n - NP) * 1024>(vq, lds_base, vvo[n - NP]);
+            }
+            if constexpr (epi) {
+                static_for<kOStores>([&](auto U) {
+                    constexpr int u = decltype(U)::value;
+                    if constexpr (2 * NP + (u * (G1 - 2 * NP)) / kOStores == g) {
+                        if (epi_pending) epi_unit(U);
+                    }
+                });
             }
             // the next block's Q: kQPT pieces per tile, in evenly spaced gaps
             if constexpr (kQL == 2 && kQPhase == 1 && do_dma && i == 3 && (ks * kQPT) % KS == 0) {
@@ -1521,7 +1589,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // are in va_pre (with SM1)
     auto phase2 = [&](const char *V, auto PPV, auto PSM, auto SM1, auto AD) __attribute__((always_inline)) {
         constexpr int cp = decltype(PPV)::value, cs = decltype(PSM)::value;
-        constexpr bool do_sm = decltype(SM1)::value;
+        constexpr bool do_sm = decltype(SM1)::value == 1;
         constexpr bool sdead = decltype(AD)::value & 1, pdead = decltype(AD)::value & 2;
         constexpr bool vpre = decltype(AD)::value & 4;  // (phase 1 read the first V^T fragments)
         u32x4 va[2][DTL];
@@ -1536,6 +1604,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             dst[n >> 1][2 * (n & 1)] = x[0];
             dst[n >> 1][2 * (n & 1) + 1] = x[1];
         };
+        constexpr bool do_late = decltype(SM1)::value == 2;  // (the drain: tile cp's late softmax)
         if constexpr (do_sm && vpre) {  // (read in phase 1 of the same iteration)
 #pragma unroll
             for (int n = 0; n < DTL; ++n) va[0][n] = va_pre[n];
@@ -1578,6 +1647,17 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                     q_piece(qnr, qn, rowB_next);
                     ++qn;
                 }
+            }
+            if constexpr (do_late && g <= 16) {
+                // late score v = g of both blocks (P of k-steps 2, 3: their MFMAs start at gap 16),
+                // the row sum and pack of score g - 1 a gap after its exp
+                static_for<2>([&](auto XX) {
+                    constexpr int X2 = decltype(XX)::value;
+                    if constexpr (!(pdead && X2 == 0)) {
+                        if constexpr (g < 16) u_exp(cp, X2, 1, g);
+                        if constexpr (g > 0) u_fin(cp, X2, 1, g - 1);
+                    }
+                });
             }
             if constexpr (do_sm) {
                 static_for<32>([&](auto M) {
@@ -1669,12 +1749,26 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         st[X].nmsc = -5.77f;
 #endif
     }
+#if FA_EPI_OVL
+    // (O is zeroed in the first tile, after the previous block's deferred epilogue has read it)
+#elif FA_ZERO_MFMA
+    zero_o();
+#else
     if constexpr (DTL == 4) fa_agpr_zero_4(); else fa_agpr_zero_2();
+#endif
     // (no pipeline fill: the block's first tile runs its own iteration without the P.V and late
-    // softmax of an empty tile -1, iter_first below)
+    // softmax of an empty tile -1, iter FIRST below)
     // Q, K_0 landed. After the first block the previous block's O stores were issued after these
     // loads: leave them in flight (vmcnt counts stores too, in issue order)
-    if (rnd == 0) dma_wait(); else __builtin_amdgcn_s_waitcnt(vmcnt_enc(kOStores));
+    // (FA_EPI_OVL: a dense block defers its stores into the next block's first tile, so only a key-split
+    // block's combining piece leaves stores in flight here)
+#ifdef FA_STAMPS
+    const uint32_t st_w0 = (uint32_t)__builtin_amdgcn_s_memtime();
+#endif
+    if (rnd == 0 || (FA_EPI_OVL && !spl)) dma_wait(); else __builtin_amdgcn_s_waitcnt(vmcnt_enc(kOStores));
+#ifdef FA_STAMPS
+    st_acc[6] = (uint32_t)__builtin_amdgcn_s_memtime() - st_w0;  // (the wait for this block's Q and K_0)
+#endif
     if (kQL && !rope_q && !q_in_agpr) q_from_lds();
     __builtin_amdgcn_s_waitcnt(kLgkm0);
     plan_next();
@@ -1743,7 +1837,10 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         static_assert(!first || (c == 1 && mk != 3), "first tile: parity 1, no previous tile");
         // (bit 2: phase 2's first V^T fragments read in phase 1 -- unmasked tiles only: in a masked one
         // they would stay live through the mask step, where the causal kernels have no VGPR to spare)
-        using AD = IC<(mk == 2 ? 1 : mk == 3 ? 3 : 0) | (mk == 0 ? 4 : 0)>;
+        using AD = IC<(mk == 2 ? 1 : mk == 3 ? 3 : 0) | (mk == 0 ? 4 : 0) | (first && FA_EPI_OVL ? 8 : 0)>;
+#if FA_EPI_OVL
+        const bool had_epi = first && epi_pending;
+#endif
         if constexpr (mk >= 2) {  // block A takes no decision and adds no row sum in tile j
             st[0].rmask = 0;
             st[0].t = 0.f;
@@ -1762,6 +1859,12 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #endif
         kp += step_k;
         vp += step_v;
+#if FA_EPI_OVL
+        if constexpr (first) {  // the previous block's O has been read: O = 0 for this block
+            zero_o();
+            epi_pending = false;
+        }
+#endif
         // the first tile's softmax reads S right after its MFMAs (no P.V MFMAs in between)
         if constexpr (first) s_ready4(S[c][0], S[c][1], S[c][2], S[c][3]);
 #ifndef FA_EXP_NOMASK  // (timing experiment of the stamps build only: no mask step, wrong results)
@@ -1794,7 +1897,12 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             rescale(false);
         }
         FA_STAMP(sc_);
+#if FA_EPI_OVL
+        // K_{j+1}, V_j landed (the first tile's pieces precede the deferred O stores: those may stay in flight)
+        if (first && had_epi) __builtin_amdgcn_s_waitcnt(vmcnt_enc(kOStores)); else dma_wait();
+#else
         dma_wait();  // K_{j+1}, V_j landed
+#endif
         FA_STAMP(sd);
         __syncthreads();
 #ifdef FA_STAMPS
@@ -1846,10 +1954,17 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     int j = jb;  // the next tile after the first
     // (the first tile computes block A even where no row of it sees a key -- key-split second pieces
     // of the first q-tiles, Sq > Sk: its scores are masked; the A-dead tiles after it run MASKED 2, 3)
-    if (j_lo < n_loop) {
-        if (j_lo < j_um || j_lo >= n_unm) iter(j_lo, IC<1>{}, IC<1>{}, IC<true>{});
-        else iter(j_lo, IC<1>{}, IC<0>{}, IC<true>{});
+    // (one body for the first tile, masked or not: its mask step masks only the wave-blocks whose rows
+    // hide a score of it, so an unmasked first tile pays the scalar tests alone -- and one body keeps
+    // the block's O zeroing on every path into the tile loops)
+    if (j_lo < n_loop) iter(j_lo, IC<1>{}, IC<1>{}, IC<true>{});
+#if FA_EPI_OVL
+    else {  // a block without tiles: the deferred stores here, then O = 0 (stored as such)
+        if (epi_pending) static_for<kOStores>([&](auto U) { epi_unit(U); });
+        zero_o();
+        epi_pending = false;
     }
+#endif
     {
         if (j_um > j) {
             const int e = min(j_um + ((j_um - j) & 1), n_loop);
@@ -1939,11 +2054,20 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         stage_k(j_lo, 1);
         if (q_in_agpr) q_from_lds();
     }
+#ifdef FA_STAMPS
+    st_acc[7] = (uint32_t)__builtin_amdgcn_s_memtime() - s_loop_end;  // (the next block's Q / K_0 issue)
+#endif
     // drain the last pipelined tile: softmax half 2 and P.V
     auto drain = [&](auto PAR, auto AD) __attribute__((always_inline)) {
         constexpr int c = decltype(PAR)::value;
-        sm2_all(PAR, AD);
-        phase2(lds + KV0 + (2 + c) * T, PAR, PAR, IC<0>{}, AD);
+        // the late scores of the last tile in the first two k-steps' MFMA gaps (their P feeds k-steps 2, 3);
+        // at D = 64 the causal kernels have no VGPRs for it (hipcc spilled into the O AGPRs)
+        if constexpr (FA_DRAIN_OVL && DTL == 4) {
+            phase2(lds + KV0 + (2 + c) * T, PAR, PAR, IC<2>{}, AD);
+        } else {
+            sm2_all(PAR, AD);
+            phase2(lds + KV0 + (2 + c) * T, PAR, PAR, IC<0>{}, AD);
+        }
     };
     if (n_loop > jlo_c) {  // (set_block above moved j_lo to the next block)
         if (kCausal && last_dead) {
@@ -2026,13 +2150,50 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             });
         });
     };
+    // (FA_SPLIT_AGPR) one block's combine from the partner records in a[PB ..): own O * fm + partner * fo,
+    // O / l, packed; the 2 * DTL store values and offsets into vals / offs
+    auto combine_block = [&](auto XX, auto PB, const float fmx, const float fox, const float inv, u32x4 *vals,
+                             int *offs) __attribute__((always_inline)) {
+        constexpr int X = decltype(XX)::value, pb = decltype(PB)::value;
+        static_for<DTL>([&](auto DD) {
+            constexpr int dt = decltype(DD)::value;
+            f32x16 od = agpr_read16<16 * DTL * X + 16 * dt>();
+            const f32x16 pw = agpr_read16<pb + 16 * dt>();
+#pragma unroll
+            for (int i = 0; i < 16; ++i) od[i] = sum_of_products(od[i], fmx, pw[i], fox);
+            const int orow = (X ? r + rowb_c : r) * os_ * 2;
+#pragma unroll
+            for (int gp = 0; gp < 4; gp += 2) {
+                const uint32_t a0 = DT::pack(od[4 * gp + 0] * inv, od[4 * gp + 1] * inv);
+                const uint32_t a1 = DT::pack(od[4 * gp + 2] * inv, od[4 * gp + 3] * inv);
+                const uint32_t b0 = DT::pack(od[4 * gp + 4] * inv, od[4 * gp + 5] * inv);
+                const uint32_t b1 = DT::pack(od[4 * gp + 6] * inv, od[4 * gp + 7] * inv);
+                const auto x0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+                const auto x1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+                const int d0 = dt * 32 + 8 * (gp + h);
+                vals[2 * dt + gp / 2] = (u32x4){x0[0], x1[0], x0[1], x1[1]};
+                offs[2 * dt + gp / 2] = (kExactD || d0 < D) ? orow + 2 * d0 : 0x7ffffff0;
+            }
+        });
+    };
     FA_STAMP(s_masked_end);
     if (!spl) {
         // row sums: each lane half summed half of the tile's keys
         const float l0 = pair_sum(st[0].l);
         const float l1 = pair_sum(st[1].l);
-        store_block(r, IC<0>{}, l0);
-        store_block(r + rowb_c, IC<16 * DTL>{}, l1);
+#if FA_EPI_OVL
+        if (more) {  // the stores go into the next block's first tile (epi_unit)
+            epi_pending = true;
+            epi_inv0 = (l0 == 0.f) ? 1.f : 1.f / l0;
+            epi_inv1 = (l1 == 0.f) ? 1.f : 1.f / l1;
+            epi_orr = orr;
+            epi_rowb = rowb_c * os_ * 2;
+        } else
+#endif
+        {
+            store_block(r, IC<0>{}, l0);
+            store_block(r + rowb_c, IC<16 * DTL>{}, l1);
+        }
     } else {
         // ---- key-split block: the two pieces meet per wave. The first to arrive leaves its
         // unnormalised O (AGPR fragment order, 64 lanes x 16 B per record) and its (nmsc, l, m) per
@@ -2081,6 +2242,15 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             }
             (void)seen;
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: loads stay below the poll)
+#if FA_SPLIT_AGPR
+            // the partner's first 16 records (block A's at D = 128, both blocks' at D = 64) into the Q AGPRs
+            // (free here: the next block's Q is read in its prologue), beside the statistics: one round trip
+            const char *wb = (const char *)(wsw + lane);
+            fa_agpr_ldws4_128(wb);
+            fa_agpr_ldws4_144(wb + 4096);
+            fa_agpr_ldws4_160(wb + 8192);
+            fa_agpr_ldws4_176(wb + 12288);
+#endif
             u32x4 s0, s1;
             ld_ws2(stats + lane, s0, s1);
             float fm[2], fo[2], lt[2];
@@ -2094,7 +2264,33 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                 fo[X] = so ? __builtin_amdgcn_exp2f(mo - mt) : 0.f;
                 lt[X] = pair_sum(sum_of_products(st[X].l, fm[X], __uint_as_float(s0[2 + X]), fo[X]));
             }
+#if FA_SPLIT_AGPR
+            const float inv0 = (lt[0] == 0.f) ? 1.f : 1.f / lt[0], inv1 = (lt[1] == 0.f) ? 1.f : 1.f / lt[1];
+            u32x4 va_[2 * DTL], vb_[2 * DTL];
+            int oa_[2 * DTL], ob_[2 * DTL];
+            if constexpr (DTL == 4) {
+                combine_block(IC<0>{}, IC<128>{}, fm[0], fo[0], inv0, va_, oa_);
+                // block B's records into the same AGPRs, then block A's stores: the counted wait below
+                // retires the loads and leaves the stores in flight
+                fa_agpr_ldws4_128(wb + 16384);
+                fa_agpr_ldws4_144(wb + 20480);
+                fa_agpr_ldws4_160(wb + 24576);
+                fa_agpr_ldws4_176(wb + 28672);
+#pragma unroll
+                for (int i = 0; i < 2 * DTL; ++i) __builtin_amdgcn_raw_buffer_store_b128(va_[i], orr, oa_[i], 0, 0);
+                asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                combine_block(IC<1>{}, IC<128>{}, fm[1], fo[1], inv1, vb_, ob_);
+            } else {
+                combine_block(IC<0>{}, IC<128>{}, fm[0], fo[0], inv0, va_, oa_);
+                combine_block(IC<1>{}, IC<160>{}, fm[1], fo[1], inv1, vb_, ob_);
+#pragma unroll
+                for (int i = 0; i < 2 * DTL; ++i) __builtin_amdgcn_raw_buffer_store_b128(va_[i], orr, oa_[i], 0, 0);
+            }
+#pragma unroll
+            for (int i = 0; i < 2 * DTL; ++i) __builtin_amdgcn_raw_buffer_store_b128(vb_[i], orr, ob_[i], 0, 0);
+#else
             store_both_combined(lt, wsw, fm, fo);
+#endif
         }
     }
 #ifdef FA_STAMPS
@@ -2105,7 +2301,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         if (stamps && lane == 0) {
             // per Q block: [total, p1, p2+rescale, dma wait, barrier, tiles, drain (+ next block's
             //  prefetch issue), prologue, epilogue, realtime (100 MHz ticks), start time, xcc, (FINE:
-            //  4 sub-phase fields), first tile]
+            //  4 sub-phase fields), prologue wait, next-block issue, first tile]
             unsigned long long *o = stamps + ((size_t)blk_c * 4 + wave) * FA_STAMP_W;
             o[0] = s_end - st_t0;
             for (int i = 0; i < 5; ++i) o[1 + i] = st_acc[i];
@@ -2119,6 +2315,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #pragma unroll
             for (int i = 0; i < 4; ++i) o[12 + i] = st_fa[i];
 #endif
+            o[FA_STAMP_W - 3] = st_acc[6];  // the prologue's wait for Q and K_0
+            o[FA_STAMP_W - 2] = st_acc[7];  // the next block's Q / K_0 issue at the block's end
             o[FA_STAMP_W - 1] = st_acc[5];  // the block's first tile (iter FIRST)
         }
     }

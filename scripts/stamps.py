@@ -7,6 +7,8 @@ bench config (DVFS settles), then one stamped launch, and prints per-wave median
 split: phase 1 (S = K.Q^T || softmax 2 || DMA), phase 2 (O += P.V || softmax 1) + rescale, the
 DMA wait, the barrier; plus the in-kernel clock (s_memtime / s_memrealtime x 100 MHz).
 usage: python scripts/stamps.py [c2|c3|c4|c5] [w4|p8]   (p8: 8 waves per Q block; p1 = phase A, p2 = B)
+env: STAMPS_SHAPE (another shape), STAMPS_WS=1 (pass the workspace: key-split causal blocks, two records
+per block), STAMPS_WIDTH (record width of the build)
 """
 import ctypes
 import os
@@ -51,9 +53,9 @@ p = P(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), cfg["B"], cfg["Hq"
       cfg["Sk"], cfg["D"], cfg["Hq"] // cfg["Hkv"],
       *[t.stride(0) for t in st], *[t.stride(1) for t in st], *[t.stride(2) for t in st],
       cfg["D"] ** -0.5 * 1.4426950408889634)
-nwg = cfg["B"] * cfg["Hq"] * ((cfg["Sq"] + 255) // 256)
-W = int(os.environ.get("STAMPS_WIDTH", "13"))  # 17: a -DFA_STAMPS_FINE build (phase sub-splits); 12 / 16: builds
-# before round 5 (no first-tile field)
+nwg = cfg["B"] * cfg["Hq"] * ((cfg["Sq"] + 255) // 256) * (2 if os.environ.get("STAMPS_WS") == "1" else 1)
+W = int(os.environ.get("STAMPS_WIDTH", "15"))  # 19: a -DFA_STAMPS_FINE build (phase sub-splits); 12 / 16: builds
+# before round 5 (no prologue-wait / next-block-issue / first-tile fields)
 buf = torch.zeros(nwg * WAVES * W, dtype=torch.int64, device=dev)
 stream = torch.cuda.current_stream().cuda_stream
 lib.fa_debug_set_stamps(ctypes.c_void_p(0))
@@ -62,17 +64,32 @@ if os.environ.get("STAMPS_ZIGZAG"):  # 0 plain causal blocks, 1 the default rule
     lib.fa_debug_set_zigzag(int(os.environ["STAMPS_ZIGZAG"]))
 import time  # noqa: E402
 
+dcode = 0 if dt == torch.float16 else 1
+ws = None
+if os.environ.get("STAMPS_WS") == "1":  # the workspace the library asks for (key-split causal blocks)
+    lib.fa_fwd_gfx950_workspace_size.restype = ctypes.c_int64
+    nws = lib.fa_fwd_gfx950_workspace_size(ctypes.byref(p), dcode, int(cfg["causal"]))
+    ws = torch.empty(max(nws, 256), dtype=torch.uint8, device=dev) if nws > 0 else None
+
+
+def launch():
+    if ws is not None:
+        rc = lib.fa_fwd_gfx950_ws(ctypes.byref(p), dcode, int(cfg["causal"]), ctypes.c_void_p(ws.data_ptr()),
+                                  ctypes.c_int64(ws.numel()), ctypes.c_void_p(stream))
+    else:
+        rc = lib.fa_fwd_gfx950(ctypes.byref(p), dcode, int(cfg["causal"]), ctypes.c_void_p(stream))
+    assert rc == 0
+
+
 t0 = time.time()
 n = 0
 while time.time() - t0 < 2.0:
-    assert lib.fa_fwd_gfx950(ctypes.byref(p), 0 if dt == torch.float16 else 1, int(cfg["causal"]),
-                             ctypes.c_void_p(stream)) == 0
+    launch()
     n += 1
     if n % 20 == 0:
         torch.cuda.synchronize()
 lib.fa_debug_set_stamps(ctypes.c_void_p(buf.data_ptr()))
-assert lib.fa_fwd_gfx950(ctypes.byref(p), 0 if dt == torch.float16 else 1, int(cfg["causal"]),
-                         ctypes.c_void_p(stream)) == 0
+launch()
 torch.cuda.synchronize()
 lib.fa_debug_set_stamps(ctypes.c_void_p(0))
 s = buf.view(-1, W).cpu().double()
@@ -85,7 +102,7 @@ for i, nm in enumerate(names):
 tiles = s[:, 5].clamp(min=1)
 for i, nm in [(1, "p1"), (2, "p2+resc"), (3, "dma_wait"), (4, "barrier")]:
     print(f"  per tile {nm:10s} {float((s[:, i] / tiles).median()):8.0f} cycles")
-if W in (16, 17):  # FA_STAMPS_FINE: phase 2 in quarters (8 of its 32 MFMA gaps each), phase 1 in halves
+if W in (16, 19):  # FA_STAMPS_FINE: phase 2 in quarters (8 of its 32 MFMA gaps each), phase 1 in halves
     q = [float((s[:, i] / tiles).median()) for i in (12, 13, 14)]
     p2t = float((s[:, 2] / tiles).median())
     h1 = float((s[:, 15] / tiles).median())
@@ -122,7 +139,8 @@ bt = torch.quantile(w0[:, 0], torch.tensor([0.1, 0.5, 0.9, 1.0], dtype=torch.flo
 btl = torch.quantile(w0[:, 5], torch.tensor([0.1, 0.5, 0.9, 1.0], dtype=torch.float64))
 print(f"  block cycles (wave 0) p10 {bt[0]:.0f}  p50 {bt[1]:.0f}  p90 {bt[2]:.0f}  max {bt[3]:.0f}; "
       f"tiles p10 {btl[0]:.0f}  p50 {btl[1]:.0f}  p90 {btl[2]:.0f}  max {btl[3]:.0f}")
-fields = [(6, "drain"), (7, "prologue"), (8, "epilogue")] + ([(W - 1, "first tile")] if W in (13, 17) else [])
+fields = [(6, "drain"), (7, "prologue"), (8, "epilogue")] + (
+    [(W - 3, "pro. wait"), (W - 2, "next issue"), (W - 1, "first tile")] if W in (15, 19) else [])
 for i, nm in fields:
     qs = torch.quantile(s[:, i], torch.tensor([0.1, 0.5, 0.9, 0.99], dtype=torch.float64))
     print(f"  {nm:10s} p10 {qs[0]:8.0f}  p50 {qs[1]:8.0f}  p90 {qs[2]:8.0f}  p99 {qs[3]:8.0f}")

@@ -423,6 +423,16 @@ def test_mfma_hazard_rules_on_synthetic_streams():
            ".LBB0_5:\n\tv_accvgpr_read_b32 v50, a0\n\ts_endpgm\n"
            ".LBB0_9:\n\tv_mov_b32_e32 v4, 0\n" + asm(f"{mf} a[0:15], v[4:7], v[8:11], a[0:15]") + "\ts_nop 15\n\ts_branch .LBB0_5\n")
     assert [h.split(": ")[1][:2] for h in A.hazards(k + far + ".Lfunc_end0:\n")] == ["R1"]
+    # hipcc's structurised joins: a flag pair set to -1 / 0 on the incoming edges and tested after the join.
+    # The accumulating MFMA is reached only on the edge that zeroed O (flag 0): no R5; with the flag
+    # values swapped the stale path is feasible and R5 fires
+    def joined(flag_zeroed, flag_skipped):
+        return ("\ts_cbranch_scc1 .LBB0_2\n" + zero16 + f"\ts_mov_b64 s[68:69], {flag_zeroed}\n\ts_branch .LBB0_3\n"
+                f".LBB0_2:\n\tv_accvgpr_read_b32 v50, a0\n\ts_mov_b64 s[68:69], {flag_skipped}\n"
+                ".LBB0_3:\n\ts_and_b64 vcc, exec, s[68:69]\n\ts_cbranch_vccz .LBB0_4\n\ts_endpgm\n"
+                ".LBB0_4:\n\ts_nop 1\n" + asm(f"{mf} a[0:15], v[4:7], v[8:11], a[0:15]"))
+    assert run(joined(0, -1)) == []
+    assert any("R5" in h for h in run(joined(-1, 0)))
 
 
 def test_mfma_hazard_gate_passes_the_product_assembly():
