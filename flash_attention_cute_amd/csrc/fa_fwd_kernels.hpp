@@ -2242,7 +2242,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             }
             (void)seen;
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: loads stay below the poll)
-#if FA_SPLIT_AGPR
+#if FA_SPLIT_AGPR && FA_QLDS != 2  // (staging 2 may have read the next block's Q into those AGPRs already)
             // the partner's first 16 records (block A's at D = 128, both blocks' at D = 64) into the Q AGPRs
             // (free here: the next block's Q is read in its prologue), beside the statistics: one round trip
             const char *wb = (const char *)(wsw + lane);
@@ -2264,7 +2264,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                 fo[X] = so ? __builtin_amdgcn_exp2f(mo - mt) : 0.f;
                 lt[X] = pair_sum(sum_of_products(st[X].l, fm[X], __uint_as_float(s0[2 + X]), fo[X]));
             }
-#if FA_SPLIT_AGPR
+#if FA_SPLIT_AGPR && FA_QLDS != 2
             const float inv0 = (lt[0] == 0.f) ? 1.f : 1.f / lt[0], inv1 = (lt[1] == 0.f) ? 1.f : 1.f / lt[1];
             u32x4 va_[2 * DTL], vb_[2 * DTL];
             int oa_[2 * DTL], ob_[2 * DTL];

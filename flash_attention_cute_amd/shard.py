@@ -71,7 +71,8 @@ def sharded_forward(q, k, v, rank: int, world: int, fn: Callable, **kw):
     """Run ``fn(q_view, k_view, v_view, **kw)`` over this rank's runs.
 
     ``q`` [B, Hq, Sq, D], ``k``/``v`` [B, Hkv, Sk, D] (any strides). Returns [(Run, out)] with
-    ``out`` [1, (h1-h0)*g, Sq, D]. Views only: the op reads the shard in place.
+    ``out`` [b_end - b, (h1-h0)*g, Sq, D]: a run spans batch rows b .. b_end - 1 (one row, or whole rows of
+    every kv-head). Views only: the op reads the shard in place.
     """
     B, Hq = q.shape[0], q.shape[1]
     Hkv = k.shape[1]

@@ -33,6 +33,15 @@ if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
     fetch = mean["FETCH_SIZE"] * 1024 * 2
     write = mean["WRITE_SIZE"] * 1024
     res.update({"fetch_bytes_corrected": fetch, "write_bytes": write, "hbm_bytes_per_launch": fetch + write})
+if "TCC_HIT_sum" in mean and "TCC_MISS_sum" in mean:
+    res["l2_hit_rate"] = mean["TCC_HIT_sum"] / max(1.0, mean["TCC_HIT_sum"] + mean["TCC_MISS_sum"])
+if "TCC_EA0_RDREQ_sum" in mean and "TCC_EA0_RDREQ_DRAM_sum" in mean:
+    # the L2's memory-side read requests (FETCH_SIZE counts them all, Infinity-Cache hits included) and
+    # the share of them the fabric sends on to DRAM
+    res["rdreq_dram_frac"] = mean["TCC_EA0_RDREQ_DRAM_sum"] / max(1.0, mean["TCC_EA0_RDREQ_sum"])
+    if "fetch_bytes_corrected" in res:
+        res["fetch_bytes_dram"] = res["fetch_bytes_corrected"] * res["rdreq_dram_frac"]
+        res["hbm_bytes_per_launch_dram"] = res["fetch_bytes_dram"] + res["write_bytes"]
 if "GRBM_GUI_ACTIVE" in mean:
     res["xcd_active_cycles"] = mean["GRBM_GUI_ACTIVE"] / 8
 if "SQ_VALU_MFMA_BUSY_CYCLES" in mean and "GRBM_GUI_ACTIVE" in mean:
