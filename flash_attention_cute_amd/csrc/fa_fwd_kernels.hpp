@@ -177,6 +177,12 @@ __device__ __forceinline__ float sum_of_products(float a, float fa, float b, flo
     asm volatile("" : "+v"(x), "+v"(y));
     return x + y;
 }
+// the same for two neighbouring elements at once (v_pk_mul_f32 x 2, v_pk_add_f32)
+__device__ __forceinline__ f32x2 sum_of_products2(f32x2 a, f32x2 fa, f32x2 b, f32x2 fb) {
+    f32x2 x = a * fa, y = b * fb;
+    asm volatile("" : "+v"(x), "+v"(y));
+    return x + y;
+}
 // Key-split workspace accesses. The two pieces of a block run on ONE XCD: fa_fwd_w4's work order puts
 // both in the list of the XCD that blockIdx & 7 names, and the hardware deals workgroups to XCDs
 // round-robin by workgroup id (MI355X_MICROARCH "Workgroup dispatch"). The hand-off relies on that
@@ -942,6 +948,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #endif
 #ifndef FA_SPLIT_AGPR  // key-split combine: partner records into the Q AGPRs, a block per round trip
 #define FA_SPLIT_AGPR 1  // (0: one d-tile of both blocks per round trip, into VGPRs)
+#endif
+#ifndef FA_SPLIT_PK  // (FA_SPLIT_AGPR) packed f32 combine with 1 / l folded into the two factors:
+#define FA_SPLIT_PK 1   // o * (fm / l) + p * (fo / l), still symmetric in the pieces (0: (o fm + p fo) / l)
 #endif
     // Q staging (kQL): 0 = HBM -> AGPR loads issued under the previous block's drain; 1 = LDS-DMA
     // into a Q image (K's swizzle) under the drain, read into the AGPRs at the block prologue;
@@ -2162,15 +2171,27 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             constexpr int dt = decltype(DD)::value;
             f32x16 od = agpr_read16<16 * DTL * X + 16 * dt>();
             const f32x16 pw = agpr_read16<pb + 16 * dt>();
+            const int orow = (X ? r + rowb_c : r) * os_ * 2;
+#if FA_SPLIT_PK
+            const f32x2 fm2 = {fmx * inv, fmx * inv}, fo2 = {fox * inv, fox * inv};
+#pragma unroll
+            for (int i = 0; i < 16; i += 2) {
+                const f32x2 c = sum_of_products2((f32x2){od[i], od[i + 1]}, fm2, (f32x2){pw[i], pw[i + 1]}, fo2);
+                od[i] = c[0];
+                od[i + 1] = c[1];
+            }
+            constexpr float sc = 1.f;
+#else
 #pragma unroll
             for (int i = 0; i < 16; ++i) od[i] = sum_of_products(od[i], fmx, pw[i], fox);
-            const int orow = (X ? r + rowb_c : r) * os_ * 2;
+            const float sc = inv;
+#endif
 #pragma unroll
             for (int gp = 0; gp < 4; gp += 2) {
-                const uint32_t a0 = DT::pack(od[4 * gp + 0] * inv, od[4 * gp + 1] * inv);
-                const uint32_t a1 = DT::pack(od[4 * gp + 2] * inv, od[4 * gp + 3] * inv);
-                const uint32_t b0 = DT::pack(od[4 * gp + 4] * inv, od[4 * gp + 5] * inv);
-                const uint32_t b1 = DT::pack(od[4 * gp + 6] * inv, od[4 * gp + 7] * inv);
+                const uint32_t a0 = DT::pack(od[4 * gp + 0] * sc, od[4 * gp + 1] * sc);
+                const uint32_t a1 = DT::pack(od[4 * gp + 2] * sc, od[4 * gp + 3] * sc);
+                const uint32_t b0 = DT::pack(od[4 * gp + 4] * sc, od[4 * gp + 5] * sc);
+                const uint32_t b1 = DT::pack(od[4 * gp + 6] * sc, od[4 * gp + 7] * sc);
                 const auto x0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
                 const auto x1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
                 const int d0 = dt * 32 + 8 * (gp + h);
