@@ -2201,6 +2201,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         });
     };
     FA_STAMP(s_masked_end);
+    [[maybe_unused]] int split_role = 0;  // (stamps) key-split piece: 1 the first to arrive, 3 the second
     if (!spl) {
         // row sums: each lane half summed half of the tile's keys
         const float l0 = pair_sum(st[0].l);
@@ -2246,7 +2247,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             st_ws(stats + 64 + lane, (u32x4){__float_as_uint(st[0].m), __float_as_uint(st[1].m), 0u, 0u});
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (every lane's records written through before the flag)
             if (lane == 0) __hip_atomic_store(sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            split_role = 1;
         } else {
+            split_role = 3;
             // bounded poll (~1 s), so a protocol failure never hangs the GPU; a timeout is counted in
             // the device's error counter (fa_split_errors) -- the rows it combines are wrong
             uint32_t seen = 1;
@@ -2334,7 +2337,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             o[8] = s_end - s_masked_end;
             o[9] = rt_end - st_rt0;
             o[10] = st_rt0;  // (realtime: one clock for every XCD)
-            o[11] = xcc_id();
+            o[11] = xcc_id() | (split_role << 8);  // (key-split role: split_role)
 #ifdef FA_STAMPS_FINE  // [12..14] phase 2 quarters 1-3 (the 4th: p2+rescale - their sum), [15] phase 1 half 1
 #pragma unroll
             for (int i = 0; i < 4; ++i) o[12 + i] = st_fa[i];

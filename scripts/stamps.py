@@ -128,7 +128,7 @@ first = float(w0[:, 10].min())
 print(f"  first block start spread {float(torch.quantile(w0[:, 10] - first, 0.99)) / 100:.2f} us (p99 over blocks), "
       f"last end - p50 end of the XCDs' last blocks:")
 for x in range(8):
-    sel = w0[:, 11] == x
+    sel = (w0[:, 11].long() & 255) == x
     if sel.any():
         e = t_end[sel]
         xs = w0[sel]
@@ -144,6 +144,13 @@ fields = [(6, "drain"), (7, "prologue"), (8, "epilogue")] + (
 for i, nm in fields:
     qs = torch.quantile(s[:, i], torch.tensor([0.1, 0.5, 0.9, 0.99], dtype=torch.float64))
     print(f"  {nm:10s} p10 {qs[0]:8.0f}  p50 {qs[1]:8.0f}  p90 {qs[2]:8.0f}  p99 {qs[3]:8.0f}")
+role = s[:, 11].long() >> 8  # key-split role (fa_fwd_w4 split_role): 1 the first piece to arrive, 3 the second
+for rl, nm in ((1, "1st, gave all"), (2, "1st, did A"), (3, "2nd, did both"), (4, "2nd, did B")):  # (2 / 4: the
+    # one-block-each hand-off of stamps builds from profiles/r5i_*, not kept)
+    sel = role == rl
+    if sel.any():
+        qs = torch.quantile(s[sel][:, 8], torch.tensor([0.1, 0.5, 0.9], dtype=torch.float64))
+        print(f"  epilogue of {nm:13s} ({int(sel.sum()):5d} waves) p10 {qs[0]:8.0f}  p50 {qs[1]:8.0f}  p90 {qs[2]:8.0f}")
 if WAVES == 8:  # leaders (waves 0-3) and followers (4-7) of every block
     w = torch.arange(s.shape[0]) % 8
     for nm, sel in (("leaders", w < 4), ("followers", w >= 4)):
