@@ -2,7 +2,7 @@
 # round 5, final library: GPU suite, smoke, the driver's default bench line, one GPU's share of the 2-, 4- and
 # 8-way strong split of C2 / C4 / C5 (the predicted 1 -> 8 curve), then every config's rocprofv3 kernel
 # trace + stats and PMC passes (scripts/profile.sh, incl. the L2 hit / DRAM split) and a plain bench line.
-# usage: r5_final.sh <tag> [phase: all | tests | shares | profiles]
+# usage: [CFGS="<configs to profile>"] r5_final.sh <tag> [phase: all | tests | shares | profiles]
 set -o pipefail
 TAG=${1:-r5f}; PH=${2:-all}
 cd $GRAFT_REPO_ROOT; OUT=gpurun_out/$TAG; mkdir -p $OUT
@@ -32,5 +32,5 @@ PY
   done
 fi
 if [ $PH = all ] || [ $PH = profiles ]; then
-  bash scripts/experiments/profile_all.sh $TAG "c2 c3 c4 c5 window decode decode_long decode_padded" 2>&1 | cut -c1-200
+  bash scripts/experiments/profile_all.sh $TAG "${CFGS:-c2 c3 c4 c5 window decode decode_long decode_padded}" 2>&1 | cut -c1-200
 fi
