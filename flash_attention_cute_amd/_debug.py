@@ -54,6 +54,8 @@ def lib(debug: bool = False) -> ctypes.CDLL:
         lib.fa_debug_set_zigzag.restype = None
         lib.fa_debug_set_split.argtypes = [ctypes.c_int]
         lib.fa_debug_set_split.restype = None
+        lib.fa_debug_set_split_pairs.argtypes = [ctypes.c_int]
+        lib.fa_debug_set_split_pairs.restype = None
         lib.fa_debug_last_zigzag.restype = ctypes.c_int
         lib.fa_split_errors.argtypes = [ctypes.c_int]
         lib.fa_split_errors.restype = ctypes.c_int64
@@ -107,9 +109,21 @@ def set_split(mode: int | None = None, debug: bool = False) -> None:
     lib(debug).fa_debug_set_split(-1 if mode is None else int(mode))
 
 
+def set_split_pairs(mode: int | None = None, debug: bool = False) -> None:
+    """Key-split pairs (a heavy and a light q-tile on two workgroups, one pass; fa_launch.h
+    use_split_pairs): 0 never, 1 where they fit one pass of the grid (the default); None restores it."""
+    lib(debug).fa_debug_set_split_pairs(-1 if mode is None else int(mode))
+
+
 def last_layout(debug: bool = False) -> str:
-    """Causal block layout of the last prefill launch on this thread: "plain", "zigzag" or "split"."""
-    return {0: "plain", 1: "zigzag", 2: "split"}[lib(debug).fa_debug_last_zigzag()]
+    """Causal block layout of the last prefill launch on this thread: "plain", "zigzag" or "split"
+    (key-split, as halves or as pairs: last_split_pairs)."""
+    return {0: "plain", 1: "zigzag", 2: "split", 3: "split"}[lib(debug).fa_debug_last_zigzag()]
+
+
+def last_split_pairs(debug: bool = False) -> bool:
+    """Whether the last prefill launch on this thread laid its key-split pieces out as pairs."""
+    return lib(debug).fa_debug_last_zigzag() == 3
 
 
 def forward(q, k, v, softmax_scale=None, causal=False, variant="w8", window_left=-1, w4_grid=None):

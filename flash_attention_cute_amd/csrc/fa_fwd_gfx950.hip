@@ -37,7 +37,7 @@ unsigned long long *g_stamps = nullptr;
 thread_local int g_last_path = fa::kPathNone;
 
 fa::Knobs knobs_from_env() {
-    fa::Knobs k{0, 0, 1, fa::kDecTargetWgs, fa::kDecNt, 1, 1};
+    fa::Knobs k{0, 0, 1, fa::kDecTargetWgs, fa::kDecNt, 1, 1, FA_SPLIT_PAIRS};
     if (const char *v = getenv("FA_GFX950_VARIANT"))
         k.variant = !strcmp(v, "w8") ? 1 : !strcmp(v, "w4slow") ? 2 : !strcmp(v, "p8") ? 3 : 0;
     if (const char *e = getenv("FA_W4_GRID")) k.w4_grid = atoll(e) > 0 ? atoll(e) : 0;
@@ -46,6 +46,7 @@ fa::Knobs knobs_from_env() {
     if (const char *e = getenv("FA_DEC_FLAGS")) k.dec_flags = atoi(e);
     if (const char *e = getenv("FA_ZIGZAG")) k.zigzag = atoi(e);
     if (const char *e = getenv("FA_SPLIT")) k.split = atoi(e);
+    if (const char *e = getenv("FA_SPLIT_PAIRS")) k.split_pairs = atoi(e);
 #ifdef FA_DEBUG_VARIANTS
     if (k.variant != 0)  // a debug / A-B body replaces the product kernel for the whole process: say so
         fprintf(stderr,
@@ -101,9 +102,14 @@ extern "C" int fa_debug_last_path(void) { return g_last_path; }
 extern "C" void fa_debug_set_split(int mode) {
     knobs_mut().split = mode < 0 ? env_defaults().split : mode;
 }
+// key-split pairs knob (Knobs::split_pairs, env FA_SPLIT_PAIRS): 0 never, 1 (default) where they fit
+// one pass of the grid (use_split_pairs); < 0 restores the environment / default value
+extern "C" void fa_debug_set_split_pairs(int mode) {
+    knobs_mut().split_pairs = mode < 0 ? env_defaults().split_pairs : mode;
+}
 // zigzag knob (fa_launch.h Knobs::zigzag): 0 never, 1 when the blocks fit one round, 2 always; < 0
 // restores the environment / default value. fa_debug_last_zigzag: the causal block layout of the
-// last prefill launch on this thread: 0 plain, 1 zigzag, 2 key-split.
+// last prefill launch on this thread: 0 plain, 1 zigzag, 2 key-split, 3 key-split pairs.
 extern "C" void fa_debug_set_zigzag(int mode) {
     knobs_mut().zigzag = mode < 0 ? env_defaults().zigzag : mode;
 }

@@ -276,6 +276,8 @@ __device__ __forceinline__ unsigned long long xcc_id() {
 
 struct Work {
     int qtile, hq, b;
+    int kr = 0;  // (fa_fwd_w4 key-split launches) kind | mid << 2: 0 the whole block, 1 its key tiles
+                 // [0, mid), 2 its key tiles [mid, n_end) -- a piece that meets its partner in the epilogue
 };
 template <bool kCausal>
 __device__ __forceinline__ Work decode_work(const uint32_t nwg, const uint32_t bid, const int n_qtiles, const int Hq,
@@ -949,6 +951,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 #ifndef FA_SPLIT_AGPR  // key-split combine: partner records into the Q AGPRs, a block per round trip
 #define FA_SPLIT_AGPR 1  // (0: one d-tile of both blocks per round trip, into VGPRs)
 #endif
+#ifndef FA_PAIR_SHIFT  // key-split pairs: the heavy q-tile's split point moves this many tiles towards
+#define FA_PAIR_SHIFT 2  // the workgroup that runs two blocks (its extra switch and hand-off)
+#endif
 #ifndef FA_SPLIT_PK  // (FA_SPLIT_AGPR) packed f32 combine with 1 / l folded into the two factors:
 #define FA_SPLIT_PK 1   // o * (fm / l) + p * (fo / l), still symmetric in the pieces (0: (o fm + p fo) / l)
 #endif
@@ -1003,28 +1008,71 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     const uint32_t nwg = (uint32_t)n_qtiles * (uint32_t)p.num_heads_q * (uint32_t)p.batch_size;
     const uint32_t xcd = blockIdx.x & 7, cx = blockIdx.x >> 3;
     const uint32_t gx = (gridDim.x - xcd + 7) >> 3;  // workgroups of this XCD
-    // key-split blocks (below): the XCD-aware order runs over (batch, q-head, q-tile) units, each
-    // expanded into its two pieces next to each other in ONE XCD's list -- the pieces meet through
-    // that XCD's L2
+    // key-split blocks (below): the XCD-aware order runs over units whose pieces meet in ONE XCD's
+    // list, so they meet through that XCD's L2. Plain split: a unit is a (batch, q-head, q-tile), its
+    // two pieces next to each other in the list, walked by the snake. Pairs (xa.split_pairs): a unit
+    // is a (batch, q-head, pair p) of the heavy q-tile Q - 1 - p and the light q-tile p on two
+    // neighbouring workgroups, in one pass: workgroup 2u runs tiles [mid, n_end) of the heavy q-tile,
+    // workgroup 2u + 1 its tiles [0, mid) and then the light q-tile whole, with mid putting the same
+    // work on both (a block switch and the hand-off counted as FA_PAIR_SHIFT tiles).
     const bool spl = kCausal && xa.split_ws != nullptr;
-    const uint32_t nunits = spl ? nwg >> 1 : nwg;
-    const uint32_t cnt = spl ? 2 * ((nunits - xcd + 7) >> 3) : (nwg - xcd + 7) >> 3;  // Q blocks of this XCD
+    const bool pairs = spl && xa.split_pairs != 0;
+    const int nqp = n_qtiles >> 1;  // (key-split launches: the host passes twice the plain q-tiles)
+    const uint32_t nunits = pairs ? (uint32_t)((nqp + 1) >> 1) * p.num_heads_q * p.batch_size : spl ? nwg >> 1 : nwg;
+    const uint32_t nux = (nunits - xcd + 7) >> 3;  // units of this XCD
+    const uint32_t cnt = pairs ? 2 * gx : spl ? 2 * nux : (nwg - xcd + 7) >> 3;  // Q blocks of this XCD
+    auto nend_of = [&](const int t) __attribute__((always_inline)) {  // a dense causal q-tile's key tiles
+        const int x = diag + min((t + 1) * kBlockM, Sq);
+        return min(x <= 0 ? 0 : (x + kBlockN - 1) / kBlockN, n_blocks);
+    };
+    // pairs: item k = rnd * gx + c of workgroup c; false if it has none
+    auto pair_item = [&](const uint32_t k, Work &w) __attribute__((always_inline)) {
+        const uint32_t r = k >= gx ? 1u : 0u, c = k - r * gx;
+        if (c >= 2 * nux) return false;
+        w = decode_work<kCausal>(nunits, xcd + 8 * (c >> 1), (nqp + 1) >> 1, (int)p.num_heads_q,
+                                 (int)p.head_q_per_group);
+        const int pl = w.qtile, hv = nqp - 1 - pl;  // light and heavy q-tile (equal: the middle one)
+        const int ch = nend_of(hv);
+        const int mid = hv == pl ? ch >> 1 : max(0, ((ch - nend_of(pl)) >> 1) - FA_PAIR_SHIFT);
+        if (!(c & 1)) {
+            w.qtile = hv;
+            w.kr = mid > 0 ? 2 | (mid << 2) : 0;
+            return r == 0;
+        }
+        const int n1 = (mid > 0 ? 1 : 0) + (hv != pl ? 1 : 0);
+        if ((int)r >= n1) return false;
+        const bool piece = r == 0 && mid > 0;
+        w.qtile = piece ? hv : pl;
+        w.kr = piece ? 1 | (mid << 2) : 0;
+        return true;
+    };
+    auto valid = [&](const uint32_t k) __attribute__((always_inline)) {
+        Work w;
+        return pairs ? pair_item(k, w) : k < cnt;
+    };
     auto work_of = [&](const uint32_t k) __attribute__((always_inline)) {
         if (!spl)
             return decode_work<kCausal>(nwg, xcd + 8 * k, n_qtiles, (int)p.num_heads_q, (int)p.head_q_per_group);
-        Work w = decode_work<kCausal>(nunits, xcd + 8 * (k >> 1), n_qtiles >> 1, (int)p.num_heads_q,
-                                      (int)p.head_q_per_group);
-        w.qtile = 2 * w.qtile + (int)(k & 1);  // (item 2t + piece)
+        Work w;
+        if (pairs) {
+            pair_item(k, w);
+        } else {
+            w = decode_work<kCausal>(nunits, xcd + 8 * (k >> 1), nqp, (int)p.num_heads_q, (int)p.head_q_per_group);
+            w.kr = (k & 1 ? 2 : 1) | ((nend_of(w.qtile) >> 1) << 2);  // piece k & 1 of the halves
+        }
         // (wave-uniform: said so, or the block's buffer descriptors may land in VGPRs, which the
         // LDS-DMA asm cannot take)
         w.qtile = __builtin_amdgcn_readfirstlane(w.qtile);
         w.hq = __builtin_amdgcn_readfirstlane(w.hq);
         w.b = __builtin_amdgcn_readfirstlane(w.b);
+        w.kr = __builtin_amdgcn_readfirstlane(w.kr);
         return w;
     };
-    auto block_of = [&](const uint32_t rnd) { return rnd * gx + ((rnd & 1) ? gx - 1 - cx : cx); };
+    auto block_of = [&](const uint32_t rnd) {
+        return pairs ? rnd * gx + cx : rnd * gx + ((rnd & 1) ? gx - 1 - cx : cx);
+    };
     uint32_t rnd = 0, kblk = block_of(0);
-    if (kblk >= cnt) return;
+    if (!valid(kblk)) return;
 
     // Zigzag Q blocks (xa.zigzag, dense causal launches whose blocks fit one round of the grid):
     // block t pairs the 128-row segment t (block A) with segment nseg - 1 - t (block B), so every
@@ -1039,8 +1087,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // neighbours of one XCD's list, so the persistent snake puts a heavy piece and a light one on
     // every workgroup (two rounds) and no block is longer than half the longest q-tile. Their
     // combine is in the epilogue.
-    auto qtile_of = [&](const Work &wk) { return spl ? wk.qtile >> 1 : wk.qtile; };
+    auto qtile_of = [&](const Work &wk) { return wk.qtile; };
     int split_slot = 0;  // (batch, q-head, plain q-tile) of the current block: its workspace slot
+    bool blk_split = false;  // the current block is a key-split piece
     auto geom_of = [&](const int qtile, const int sq, int &m0o, int &rowbo) __attribute__((always_inline)) {
         if (zz) {
             const int nseg = (sq + 127) >> 7, sB = nseg - 1 - qtile;
@@ -1117,12 +1166,16 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             j_lo = min(max(lo0, 0) / kBlockN, n_end);
             j_um = min((max(lo1, 0) + kBlockN - 1) / kBlockN, n_end);
         }
-        if (spl) {  // piece 0: tiles [0, mid); piece 1: [mid, n_end), the diagonal tiles among them
-            const int mid = n_end / 2;
-            if (wk.qtile & 1) j_lo = j_um = mid;
-            else n_end = mid;
+        if (spl) {  // a piece: tiles [0, mid) (kind 1) or [mid, n_end) (kind 2, the diagonal tiles among them)
+            const int kind = wk.kr & 3, mid = wk.kr >> 2;
+            // (selects, not branches: a three-way branch here let hipcc move the K / V tile descriptors
+            // into VGPRs, which the LDS-DMA asm cannot take)
+            j_lo = kind == 2 ? mid : j_lo;
+            j_um = kind == 2 ? mid : j_um;
+            n_end = kind == 1 ? mid : n_end;
             n_pipe = min(n_pipe, n_end);
-            split_slot = (b * (int)p.num_heads_q + hq) * (n_qtiles >> 1) + (wk.qtile >> 1);
+            blk_split = kind != 0;
+            split_slot = (b * (int)p.num_heads_q + hq) * nqp + wk.qtile;
         }
     };
     set_block(work_of(kblk));
@@ -1211,7 +1264,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         const uint32_t kn = block_of(rnd + 1);
         qn = 0;
         qnt = 0;
-        if (kn < cnt) {
+        if (valid(kn)) {
             wk_next = work_of(kn);
             if (kQL && !rope_q) {
                 qnr = q_rsrc_of(wk_next, rowB_next);
@@ -2047,11 +2100,12 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // drain reads only a V slot).
     char *const ob_c = ob;
     const int mw_c = mw, sq_c = Sq, jlo_c = j_lo, rowb_c = rowB, slot_c = split_slot;
+    const bool spl_c = blk_split;
 #ifdef FA_STAMPS
     const uint32_t blk_c = xcd + 8 * kblk;
 #endif
     kblk = block_of(++rnd);
-    const bool more = kblk < cnt;
+    const bool more = valid(kblk);
     if (more) {
         set_block(wk_next);
         // kQL: when this block's tiles issued all the next block's Q pieces they have landed (each
@@ -2202,7 +2256,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     };
     FA_STAMP(s_masked_end);
     [[maybe_unused]] int split_role = 0;  // (stamps) key-split piece: 1 the first to arrive, 3 the second
-    if (!spl) {
+    if (!spl_c) {
         // row sums: each lane half summed half of the tile's keys
         const float l0 = pair_sum(st[0].l);
         const float l1 = pair_sum(st[1].l);
@@ -2378,6 +2432,8 @@ int launch_one(const fa_fwd_params &p, const PathArgs &xa, hipStream_t stream) {
     if (variant == 1) xz.split_ws = nullptr;
     xz.zigzag = !xz.split_ws && variant != 1 && use_zigzag(p, C, xa) ? 1 : 0;
     const int64_t n_plain = (p.seqlen_q + kBlockM - 1) / kBlockM;
+    xz.split_pairs = xz.split_ws && use_split_pairs(p, device_cus()) ? 1 : 0;
+    const int64_t n_pairs = (n_plain + 1) / 2 * p.num_heads_q * p.batch_size;
     const int64_t n_qtiles = xz.split_ws ? 2 * n_plain : xz.zigzag ? zigzag_qtiles(p.seqlen_q) : n_plain;
     const int64_t nwg = n_qtiles * p.num_heads_q * p.batch_size;
 #ifdef FA_DEBUG_VARIANTS
@@ -2388,12 +2444,13 @@ int launch_one(const fa_fwd_params &p, const PathArgs &xa, hipStream_t stream) {
 #endif
         // persistent: about one workgroup per CU (the kernel walks the Q blocks itself)
         hipLaunchKernelGGL((fa_fwd_w4<DT, C, kD, kExact>),
-                           dim3((uint32_t)(xz.split_ws ? w4_grid_split(nwg / 2) : w4_grid(nwg))), dim3(256), 0, stream, p,
+                           dim3((uint32_t)(xz.split_ws ? w4_grid_split(xz.split_pairs ? n_pairs : nwg / 2) : w4_grid(nwg))),
+                           dim3(256), 0, stream, p,
                            (int)n_qtiles, variant == 2 ? 1 : 0, stamp_buffer(), xz);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "HIP launch failed: %s", hipGetErrorString(e));
     set_last_path(variant == 1 ? kPathW8 : variant == 2 ? kPathW4Slow : kPathW4);
-    set_last_zigzag(xz.split_ws ? 2 : xz.zigzag);
+    set_last_zigzag(xz.split_ws ? 2 + xz.split_pairs : xz.zigzag);
     return FA_OK;
 }
 

@@ -48,6 +48,7 @@ struct Knobs {
     int dec_flags;
     int zigzag;
     int split;  // key-split causal Q blocks (use_split): 0 never, 1 where measured faster (default), 2 always
+    int split_pairs;  // key-split pairs (use_split_pairs): 0 never, 1 where they fit one pass (default)
 };
 
 const Knobs &knobs();
@@ -94,6 +95,8 @@ int64_t device_cus();
 // them with its own and stores O (fa_fwd_w4 "Key-split causal blocks"). split_sync: per (block,
 // wave) [arrivals, ready] counters, zero at the launch; the combining piece zeroes its pair again
 // (split_sync_area). split_err: the device's count of hand-offs that timed out (or nullptr).
+// split_pairs (set by launch_one, use_split_pairs): the pieces are laid out as pairs of a heavy
+// and a light q-tile on two workgroups (fa_fwd_w4 "key-split blocks").
 struct PathArgs {
     const void *cos;
     const void *sin;
@@ -107,6 +110,7 @@ struct PathArgs {
     float *split_ws;
     unsigned *split_sync;
     unsigned *split_err;
+    int split_pairs;
 };
 
 // Whether a prefill launch runs zigzag Q blocks, and its logical q-tile count (blocks per (batch,
@@ -139,6 +143,23 @@ constexpr int kSplitStatsPerLane = 8;  // floats: (nmsc, l) of blocks A and B, t
 inline int64_t split_wave_floats(int64_t headdim) {
     return 64 * ((headdim <= 64 ? 2 : 4) * 32 + kSplitStatsPerLane);  // 64 lanes x (2 blocks x DTL x 16 + stats)
 }
+// Key-split pairs (fa_fwd_w4 "key-split blocks"): when the split's two pieces per block would need a
+// second round of the grid (more plain blocks than half the CUs), lay them out as pairs instead --
+// the heavy q-tile Q - 1 - p split between two workgroups, one of which then also runs the light
+// q-tile p whole -- one pass, two workgroups per pair, so the grid must hold 2 x ceil(pairs / 8) per
+// XCD. Knob split_pairs (env FA_SPLIT_PAIRS): 0 never, 1 where this holds (default).
+#ifndef FA_SPLIT_PAIRS
+#define FA_SPLIT_PAIRS 1
+#endif
+// workgroups of a key-split launch over `units` plain blocks (2 pieces each) or pairs: every XCD gets
+// two workgroups per unit of its list when that fits the grid cap (units are dealt to XCDs, so 2 *
+// units workgroups could leave some XCD short and run both pieces of a block on one workgroup)
+int64_t w4_grid_split(int64_t units);
+inline bool use_split_pairs(const fa_fwd_params &p, int64_t cus) {
+    if (knobs().split_pairs == 0) return false;
+    const int64_t nq = (p.seqlen_q + kBlockM - 1) / kBlockM, units = (nq + 1) / 2 * p.num_heads_q * p.batch_size;
+    return 2 * nq * p.num_heads_q * p.batch_size > cus && w4_grid_split(units) == 16 * ((units + 7) / 8);
+}
 inline int64_t split_blocks(const fa_fwd_params &p) {
     return (p.seqlen_q + kBlockM - 1) / kBlockM * p.num_heads_q * p.batch_size;
 }
@@ -152,10 +173,6 @@ inline int64_t split_ws_bytes(const fa_fwd_params &p) {
 // a graph before the area exists (the caller then zeroes counters in its workspace). *err: the device's
 // hand-off error counter (nullptr under capture before it exists).
 unsigned *split_sync_area(hipStream_t stream, int64_t bytes, unsigned **err);
-// workgroups of a key-split launch over `units` plain blocks (2 pieces each): every XCD gets a workgroup
-// per piece of its units when that fits the grid cap (pieces are dealt to XCDs by unit, so 2 * units
-// workgroups could leave some XCD short and run both pieces of a block on one workgroup)
-int64_t w4_grid_split(int64_t units);
 
 // launch one (dtype, causal, head-dim tile, exact head dim) instantiation on `stream`
 template <class DT, bool C, int kD, bool kExact>

@@ -406,6 +406,72 @@ def test_key_split_causal_blocks(device, shape, dtype):
     assert (out.float() - plain.float()).abs().max().item() < tol
 
 
+PAIRS = [  # (B, Hq, Hkv, Sq, Sk, D): one-round causal grids with more plain blocks than half the CUs
+    (1, 16, 4, 4096, 4096, 128),  # C4's 8-way share: 16 q-tiles per head, pairs (15, 0) .. (8, 7)
+    (1, 24, 24, 1536, 1536, 64),  # 6 q-tiles: short pairs, the split point clamps to 0 (no hand-off)
+    (1, 16, 8, 2304, 2304, 128),  # 9 q-tiles: the middle one halves over its two workgroups
+    (1, 32, 8, 1280, 2000, 128),  # Sq < Sk, 5 q-tiles
+    (2, 12, 4, 1500, 700, 64),    # Sq > Sk: the first rows see no key (output 0)
+]
+
+
+@pytest.mark.parametrize("shape", PAIRS, ids=[str(s) for s in PAIRS])
+def test_key_split_pairs(device, shape):
+    """Key-split pairs (fa_fwd_w4 "key-split blocks", fa_launch.h use_split_pairs): the heavy q-tile
+    Q - 1 - p split between two workgroups, one of which also runs the light q-tile p. Against the
+    oracle, two launches bit-identical, close to the plain layout and to the halves layout
+    (different split points: summation order only), no hand-off error; a capped grid (no room for a
+    pass) falls back to the halves."""
+    import flash_attention_cute_amd as m
+    from flash_attention_cute_amd import _debug
+
+    b, hq, hkv, sq, sk, d = shape
+    dtype = torch.float16
+    seed = zlib.crc32(repr((shape, "pairs")).encode())
+    q, k, v = make(b, hq, hkv, sq, sk, d, dtype, seed)
+    qd, kd, vd = q.to(device), k.to(device), v.to(device)
+    _debug.set_knobs()
+    _debug.set_split(2)
+    m.split_errors(reset=True)
+    try:
+        out = m.flash_attn_func(qd, kd, vd, causal=True)
+        assert _debug.last_layout() == "split" and _debug.last_split_pairs()
+        again = m.flash_attn_func(qd, kd, vd, causal=True)
+        _debug.set_split_pairs(0)
+        halves = m.flash_attn_func(qd, kd, vd, causal=True)
+        assert _debug.last_layout() == "split" and not _debug.last_split_pairs()
+        _debug.set_split_pairs()
+        with _debug.knobs(w4_grid=64):
+            capped = m.flash_attn_func(qd, kd, vd, causal=True)
+            assert _debug.last_layout() == "split" and not _debug.last_split_pairs()
+        _debug.set_split(0)
+        _debug.set_zigzag(0)
+        plain = m.flash_attn_func(qd, kd, vd, causal=True)
+        torch.cuda.synchronize()
+    finally:
+        _debug.set_split()
+        _debug.set_split_pairs()
+        _debug.set_zigzag()
+    assert m.split_errors() == 0
+    assert torch.equal(out, again) and torch.equal(halves, capped)
+    check(out, q, k, v, d ** -0.5, True, dtype)
+    for other in (plain, halves):
+        assert (out.float() - other.float()).abs().max().item() < 4e-3
+
+
+def test_key_split_pairs_by_default_on_the_c4_share(device):
+    """The default rule sends C4's 8-way share (B1 Hq16 Hkv4 S4096 causal) to key-split pairs."""
+    import flash_attention_cute_amd as m
+    from flash_attention_cute_amd import _debug
+
+    q, k, v = (torch.randn(1, h, 4096, 128, device=device, dtype=torch.float16) for h in (16, 4, 4))
+    _debug.set_knobs()
+    _debug.set_split()
+    _debug.set_split_pairs()
+    m.flash_attn_func(q, k, v, causal=True)
+    assert _debug.last_layout() == "split" and _debug.last_split_pairs()
+
+
 def test_key_split_only_with_a_workspace(device):
     """The C-ABI runs key-split blocks only when the caller passes the workspace
     fa_fwd_gfx950_workspace_size asks for (the torch op does); without one (plain fa_fwd_gfx950) the
