@@ -2276,13 +2276,16 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     } else {
         // ---- key-split block: the two pieces meet per wave. The first to arrive leaves its
         // unnormalised O (AGPR fragment order, 64 lanes x 16 B per record) and its (nmsc, l, m) per
-        // lane in the workspace and raises the ready flag; the second waits for that flag (the first
-        // has finished its tiles and only stores), rescales both to their larger reference and stores
-        // O. (The pieces run on one XCD by work_of's order; the accesses do not rely on it.)
+        // lane in the workspace and marks them ready in the arrivals word; the second finds them
+        // ready in its own arrival, or waits for the mark (the first has finished its tiles and only
+        // stores), rescales both to their larger reference and stores O. (The pieces run on one XCD
+        // by work_of's order; the accesses do not rely on it.)
         constexpr int kWaveF = 64 * (32 * DTL + kSplitStatsPerLane);
         unsigned *sync = xa.split_sync + 2 * ((size_t)slot_c * 4 + wave);
         u32x4 *wsw = (u32x4 *)(xa.split_ws + ((size_t)slot_c * 4 + wave) * kWaveF);
         u32x4 *stats = wsw + 8 * DTL * 64;  // after the 2 x DTL x 4 O records
+        // sync[0]: arrivals + kReady once the first piece's records are written (sync[1] is unused)
+        constexpr uint32_t kReady = 4;
         uint32_t arrived = 0;
         if (lane == 0) arrived = __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         arrived = __builtin_amdgcn_readfirstlane(arrived);
@@ -2300,28 +2303,25 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                                         __float_as_uint(st[0].l), __float_as_uint(st[1].l)});
             st_ws(stats + 64 + lane, (u32x4){__float_as_uint(st[0].m), __float_as_uint(st[1].m), 0u, 0u});
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (every lane's records written through before the flag)
-            if (lane == 0) __hip_atomic_store(sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // ready: + kReady on the arrivals word (an add: the partner's arrival may land in between)
+            if (lane == 0) __hip_atomic_fetch_add(sync, kReady, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             split_role = 1;
         } else {
             split_role = 3;
-            // bounded poll (~1 s), so a protocol failure never hangs the GPU; a timeout is counted in
-            // the device's error counter (fa_split_errors) -- the rows it combines are wrong
-            uint32_t seen = 1;
+            // the arrival already saw the records ready (the pairs layout's usual case: the partner
+            // finished long before), or a bounded poll (~1 s), so a protocol failure never hangs the
+            // GPU; a timeout is counted in the device's error counter (fa_split_errors) -- the rows it
+            // combines are wrong
             if (lane == 0) {
-                seen = 0;
-                for (int it = 0; it < (1 << 22); ++it) {
-                    if (__hip_atomic_load(sync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
-                        seen = 1;
-                        break;
-                    }
+                bool seen = arrived >= kReady;
+                for (int it = 0; !seen && it < (1 << 22); ++it) {
                     __builtin_amdgcn_s_sleep(8);
+                    seen = __hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= kReady;
                 }
                 if (!seen && xa.split_err) __hip_atomic_fetch_add(xa.split_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 // both pieces are past their last access to the pair: zero it for the next launch
                 __hip_atomic_store(sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            (void)seen;
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: loads stay below the poll)
 #if FA_SPLIT_AGPR && FA_QLDS != 2  // (staging 2 may have read the next block's Q into those AGPRs already)
             // the partner's first 16 records (block A's at D = 128, both blocks' at D = 64) into the Q AGPRs

@@ -93,7 +93,8 @@ int64_t device_cus();
 // block runs as two pieces over the two halves of its key tiles, on two workgroups; the piece that
 // finishes first leaves its unnormalised O and row statistics in split_ws, the second combines
 // them with its own and stores O (fa_fwd_w4 "Key-split causal blocks"). split_sync: per (block,
-// wave) [arrivals, ready] counters, zero at the launch; the combining piece zeroes its pair again
+// wave) [arrivals + 4 once the first piece's records are ready, unused] words, zero at the launch;
+// the combining piece zeroes its pair again
 // (split_sync_area). split_err: the device's count of hand-offs that timed out (or nullptr).
 // split_pairs (set by launch_one, use_split_pairs): the pieces are laid out as pairs of a heavy
 // and a light q-tile on two workgroups (fa_fwd_w4 "key-split blocks").
