@@ -161,6 +161,39 @@ def test_reference_golden_gqa128_vectors_on_gpu(op, device):
     assert m.split_errors() == 0
 
 
+def test_reference_golden_pairs_on_gpu(op, device):
+    """Key-split PAIRS pinned to the REFERENCE's outputs (golden_pairs.npz): fp16 causal B1 Hq12 Hkv3
+    S3072 D128, 144 Q blocks that the default rule lays out as pairs of a heavy and a light q-tile on
+    two workgroups; the reference's rows of three q-heads (every 8th row)."""
+    import sys
+
+    import flash_attention_cute_amd as m
+    from flash_attention_cute_amd import _debug
+
+    sys.path.insert(0, str(GOLD))
+    from make_golden import pairs_codes
+
+    g = np.load(GOLD / "golden_pairs.npz")
+    assert json.loads((GOLD / "golden_meta.json").read_text())["n_pairs_cases"] == 1
+    b, hq, hkv, sq, sk, d, causal = (int(x) for x in g["meta"])
+    cs = float(g["code_scale"])
+    q, k, v = (torch.from_numpy(c).to(torch.float16).div_(cs).to(device)
+               for c in pairs_codes(int(g["seed"]), b, hq, hkv, sq, sk, d))
+    _debug.set_knobs()
+    _debug.set_split()
+    _debug.set_split_pairs()
+    m.split_errors(reset=True)
+    out = op(q, k, v, causal=bool(causal))
+    assert _debug.last_layout() == "split" and _debug.last_split_pairs()
+    heads, rows = torch.from_numpy(g["heads"]), torch.from_numpy(g["rows"])
+    sel = out.float().cpu()[:, heads][:, :, rows]
+    ref = _gold_tensor(g["o"], "f16").float()
+    err = (sel - ref).abs()
+    assert (err <= 2e-3 + 2e-3 * ref.abs()).all(), err.max().item()
+    assert err.mean().item() < 2e-3 / 8
+    assert m.split_errors() == 0
+
+
 @pytest.mark.parametrize("causal", [False, True])
 def test_reference_module_path_pybind_call_matches_flash_attn_func(op, device, causal):
     """Code written against the reference's submodule: ``flash_attention.flash_attention

@@ -201,6 +201,35 @@ def test_golden_gqa128_cases(i):
     assert np.abs(out - o).mean() < atol / 8
 
 
+def pairs_codes(*args):
+    """golden_pairs.npz's input codes, regenerated from its seed by the generator's own function."""
+    import sys
+
+    sys.path.insert(0, str(GOLD))
+    from make_golden import pairs_codes as gen
+
+    return gen(*args)
+
+
+def test_golden_pairs_case():
+    """The key-split pairs fixture (golden_pairs.npz: the reference op on a causal GQA launch that the
+    default rule runs as pairs; inputs regenerated from the stored seed): the restatement on the three
+    sampled q-heads reproduces the reference's sampled rows."""
+    g = np.load(GOLD / "golden_pairs.npz")
+    assert json.loads((GOLD / "golden_meta.json").read_text())["n_pairs_cases"] == 1
+    b, hq, hkv, sq, sk, d, causal = (int(x) for x in g["meta"])
+    qc, kc, vc = pairs_codes(int(g["seed"]), b, hq, hkv, sq, sk, d)
+    cs, heads, rows = float(g["code_scale"]), g["heads"], g["rows"]
+    grp = hq // hkv
+    q = qc[:, heads].astype(np.float64) / cs
+    k, v = (c[:, heads // grp].astype(np.float64) / cs for c in (kc, vc))
+    out = O.flash_attention_fwd(q, k, v, float(g["scale"]), bool(causal), "f16")[:, :, rows]
+    o = as_f64(g["o"], "f16")
+    assert out.shape == o.shape
+    np.testing.assert_allclose(out, o, atol=2e-3, rtol=2e-3)
+    assert np.abs(out - o).mean() < 2e-3 / 8
+
+
 def test_golden_gqa_covers_the_pack_and_the_mapping():
     g = np.load(GOLD / "golden_gqa.npz")
     n = json.loads((GOLD / "golden_meta.json").read_text())["n_gqa_cases"]
