@@ -22,6 +22,8 @@ for f in glob.glob(f"{src}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         if any(k in r["Kernel_Name"] for k in KERNELS):
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+if not agg:  # (a missing or empty profile directory must not overwrite a good pmc_<cfg>.json)
+    sys.exit(f"pmc_to_json: no counter rows of {KERNELS} under {src}")
 mean = {k: sum(v) / len(v) for k, v in agg.items()}
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from bench import lib_sha16  # noqa: E402  (the library these passes profiled: bench.py uses the
