@@ -56,6 +56,8 @@ def lib(debug: bool = False) -> ctypes.CDLL:
         lib.fa_debug_set_split.restype = None
         lib.fa_debug_set_split_pairs.argtypes = [ctypes.c_int]
         lib.fa_debug_set_split_pairs.restype = None
+        lib.fa_debug_set_dec_fuse.argtypes = [ctypes.c_int]
+        lib.fa_debug_set_dec_fuse.restype = None
         lib.fa_debug_last_zigzag.restype = ctypes.c_int
         lib.fa_split_errors.argtypes = [ctypes.c_int]
         lib.fa_split_errors.restype = ctypes.c_int64
@@ -113,6 +115,12 @@ def set_split_pairs(mode: int | None = None, debug: bool = False) -> None:
     """Key-split pairs (a heavy and a light q-tile on two workgroups, one pass; fa_launch.h
     use_split_pairs): 0 never, 1 where they fit one pass of the grid (the default); None restores it."""
     lib(debug).fa_debug_set_split_pairs(-1 if mode is None else int(mode))
+
+
+def set_dec_fuse(mode: int | None = None, debug: bool = False) -> None:
+    """Split-KV decode merge: 1 the last split of a unit merges inside fa_decode (the default), 0 the
+    separate fa_decode_combine launch; None restores the default."""
+    lib(debug).fa_debug_set_dec_fuse(-1 if mode is None else int(mode))
 
 
 def last_layout(debug: bool = False) -> str:

@@ -54,6 +54,63 @@ struct DecGeo {
     static constexpr int kQPiecesPerWave = kDecRows * RB / 1024 / kDecWaves;  // 2 / 1
 };
 
+// Fused merge of a unit's n_split partials by the last of its workgroups (fa_decode, a.cnt): the same
+// arithmetic as fa_decode_combine (weights 2^(lse - M) in split order, acc / L), spread over the
+// workgroup: lse of every (split, row) into LDS, each row's weights by one thread, then a float4 of
+// one valid row per thread per pass. Loads are device-scope (sc1: not from this CU's L1).
+template <class DT, int kD, bool kExactD>
+__device__ __forceinline__ void decode_merge(const fa_fwd_params &p, const DecArgs &a, const int unit, const int b,
+                                          const int hkv, const int rb) {
+    __shared__ float wt[kDecMaxSplit][kDecRows];
+    __shared__ float linv[kDecRows];
+    const int tid = threadIdx.x, ns = a.n_split;
+    const size_t base = (size_t)unit * ns * kDecRows;  // slot of (split 0, row 0)
+    const int nrow = min(a.rows - rb * kDecRows, kDecRows);  // valid rows of this unit
+    const rsrc_t lr = make_rsrc((const char *)(a.ws_lse + base), (uint32_t)(ns * kDecRows * 4));
+    const rsrc_t orr = make_rsrc((const char *)(a.ws_o + base * kD), (uint32_t)(ns * kDecRows * kD * 4));
+    constexpr int kSc1 = 16;  // (CPol SC1: device scope, misses this CU's L1)
+    for (int i = tid; i < ns * kDecRows; i += 256)
+        wt[i / kDecRows][i % kDecRows] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(lr, 4 * i, 0, kSc1));
+    __syncthreads();
+    if (tid < nrow) {
+        float M = kNeg, L = 0.f;
+        for (int s = 0; s < ns; ++s) M = fmaxf(M, wt[s][tid]);
+        for (int s = 0; s < ns; ++s) {
+            const float ls = wt[s][tid];
+            const float w = (ls <= 0.5f * kNeg) ? 0.f : __builtin_amdgcn_exp2f(ls - M);
+            L += w;
+            wt[s][tid] = w;
+        }
+        linv[tid] = L > 0.f ? 1.f / L : 0.f;
+    }
+    __syncthreads();
+    constexpr int C4 = kD / 4;  // float4 chunks of a row
+    const int Sq = (int)p.seqlen_q, D = (int)p.headdim;
+    for (int it = tid; it < nrow * C4; it += 256) {
+        const int row = it / C4, c = it % C4;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 8
+        for (int s = 0; s < ns; ++s) {
+            const float w = wt[s][row];
+            const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(orr, (((s * kDecRows) + row) * kD + 4 * c) * 4, 0, kSc1);
+            acc.x += w * __uint_as_float(x[0]);
+            acc.y += w * __uint_as_float(x[1]);
+            acc.z += w * __uint_as_float(x[2]);
+            acc.w += w * __uint_as_float(x[3]);
+        }
+        const float inv = linv[row];
+        const int rg = rb * kDecRows + row;
+        const int hq = hkv * a.g + rg / Sq, pos = rg % Sq;
+        char *orow = (char *)p.o_ptr +
+                     2 * ((int64_t)b * p.o_batch_stride + (int64_t)hq * p.o_head_stride + (int64_t)pos * p.o_seqlen_stride);
+        const int d = 4 * c;
+        if (kExactD || d < D) {
+            const u32x2 w2 = {DT::pack(acc.x * inv, acc.y * inv), DT::pack(acc.z * inv, acc.w * inv)};
+            *(u32x2 *)(orow + 2 * d) = w2;
+        }
+    }
+}
+
 template <class DT, bool kCausal, int kD, bool kExactD>
 __global__ __launch_bounds__(256, 1) void fa_decode(const fa_fwd_params p, const DecArgs a) {
     using G = Geo<kD>;
@@ -65,6 +122,7 @@ __global__ __launch_bounds__(256, 1) void fa_decode(const fa_fwd_params p, const
     __shared__ __attribute__((aligned(1024))) char lds[DG::kLds];
     __shared__ __attribute__((aligned(1024))) char qlds[kDecRows * RB];
     __shared__ float ml[kDecWaves][kDecRows][2];
+    __shared__ uint32_t last_wg;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -73,8 +131,19 @@ __global__ __launch_bounds__(256, 1) void fa_decode(const fa_fwd_params p, const
     const int h = lane >> 5;
 
     // ---- work: (unit = (b, hkv, rb), split) ----------------------------------------------------
-    const int split = blockIdx.x % a.n_split;
-    const int unit = blockIdx.x / a.n_split;
+    // fused merge (a.cnt): unit u's splits are the workgroups (u >> 3) * n_split + split of XCD u & 7
+    // (the hardware deals workgroups to XCDs by id mod 8), so the last one reads the others' partials
+    // through its own L2; the grid pads every XCD to the same count (the extra workgroups leave)
+    int split, unit;
+    if (a.cnt) {
+        const int k = (int)(blockIdx.x >> 3);
+        unit = ((k / a.n_split) << 3) | (int)(blockIdx.x & 7);
+        split = k % a.n_split;
+        if (unit >= (int)p.batch_size * (int)p.num_heads_kv * a.n_rb) return;
+    } else {
+        split = blockIdx.x % a.n_split;
+        unit = blockIdx.x / a.n_split;
+    }
     const int rb = unit % a.n_rb;
     const int hkv = (unit / a.n_rb) % (int)p.num_heads_kv;
     const int b = unit / (a.n_rb * (int)p.num_heads_kv);
@@ -326,13 +395,29 @@ __global__ __launch_bounds__(256, 1) void fa_decode(const fa_fwd_params p, const
                 }
             }
         }
-    } else if (rg2 < a.rows) {
-        const size_t slot = (size_t)blockIdx.x * kDecRows + row;  // (unit * n_split + split) * 32 + row
-        float *dst = a.ws_o + slot * kD + part * DPT;
+    } else {
+        if (rg2 < a.rows) {
+            const size_t slot = ((size_t)unit * a.n_split + split) * kDecRows + row;
+            float *dst = a.ws_o + slot * kD + part * DPT;
 #pragma unroll
-        for (int i = 0; i < DPT; i += 4)
-            *(float4 *)(dst + i) = make_float4(acc[i] * inv, acc[i + 1] * inv, acc[i + 2] * inv, acc[i + 3] * inv);
-        if (part == 0) a.ws_lse[slot] = L > 0.f ? M + __builtin_amdgcn_logf(L) : kNeg;  // log2
+            for (int i = 0; i < DPT; i += 4)
+                *(float4 *)(dst + i) = make_float4(acc[i] * inv, acc[i + 1] * inv, acc[i + 2] * inv, acc[i + 3] * inv);
+            if (part == 0) a.ws_lse[slot] = L > 0.f ? M + __builtin_amdgcn_logf(L) : kNeg;  // log2
+        }
+        if (a.cnt) {
+            // fused merge: every thread's partials are in L2 before the workgroup arrives; the last
+            // arrival merges the unit (the others' stores were drained before their arrivals, and
+            // its loads bypass its CU's L1)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) {
+                const uint32_t old = __hip_atomic_fetch_add(a.cnt + unit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                last_wg = old + 1 == (uint32_t)a.n_split;
+                if (last_wg) __hip_atomic_store(a.cnt + unit, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __syncthreads();
+            if (last_wg) decode_merge<DT, kD, kExactD>(p, a, unit, b, hkv, rb);
+        }
     }
 }
 
@@ -396,8 +481,14 @@ int launch_decode(const fa_fwd_params &p, DecArgs a, void *ws, hipStream_t strea
         a.ws_o = (float *)ws;
         a.ws_lse = (float *)((char *)ws + slots * kD * 4);
     }
-    hipLaunchKernelGGL((fa_decode<DT, C, kD, kExact>), dim3((uint32_t)(units * a.n_split)), dim3(256), 0, stream, p, a);
-    if (a.n_split > 1)
+    if (a.n_split > 1 && knobs().dec_fuse) {  // fused merge: the stream's zeroed per-unit counters, if any
+        unsigned *err = nullptr;
+        a.cnt = split_sync_area(stream, units * 4, &err);
+    }
+    // (fused: every XCD holds ceil(units / 8) units' splits)
+    const int64_t grid = a.cnt ? 8 * ((units + 7) / 8) * a.n_split : units * a.n_split;
+    hipLaunchKernelGGL((fa_decode<DT, C, kD, kExact>), dim3((uint32_t)grid), dim3(256), 0, stream, p, a);
+    if (a.n_split > 1 && !a.cnt)
         hipLaunchKernelGGL((fa_decode_combine<DT, kD, kExact>),
                            dim3((uint32_t)(p.batch_size * p.num_heads_kv * ((a.rows + 3) / 4))), dim3(256), 0, stream,
                            p, a);

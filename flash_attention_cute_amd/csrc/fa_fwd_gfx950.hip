@@ -37,7 +37,7 @@ unsigned long long *g_stamps = nullptr;
 thread_local int g_last_path = fa::kPathNone;
 
 fa::Knobs knobs_from_env() {
-    fa::Knobs k{0, 0, 1, fa::kDecTargetWgs, fa::kDecNt, 1, 1, FA_SPLIT_PAIRS};
+    fa::Knobs k{0, 0, 1, fa::kDecTargetWgs, fa::kDecNt, 1, 1, FA_SPLIT_PAIRS, FA_DEC_FUSE};
     if (const char *v = getenv("FA_GFX950_VARIANT"))
         k.variant = !strcmp(v, "w8") ? 1 : !strcmp(v, "w4slow") ? 2 : !strcmp(v, "p8") ? 3 : 0;
     if (const char *e = getenv("FA_W4_GRID")) k.w4_grid = atoll(e) > 0 ? atoll(e) : 0;
@@ -47,6 +47,7 @@ fa::Knobs knobs_from_env() {
     if (const char *e = getenv("FA_ZIGZAG")) k.zigzag = atoi(e);
     if (const char *e = getenv("FA_SPLIT")) k.split = atoi(e);
     if (const char *e = getenv("FA_SPLIT_PAIRS")) k.split_pairs = atoi(e);
+    if (const char *e = getenv("FA_DEC_FUSE")) k.dec_fuse = atoi(e);
 #ifdef FA_DEBUG_VARIANTS
     if (k.variant != 0)  // a debug / A-B body replaces the product kernel for the whole process: say so
         fprintf(stderr,
@@ -106,6 +107,11 @@ extern "C" void fa_debug_set_split(int mode) {
 // one pass of the grid (use_split_pairs); < 0 restores the environment / default value
 extern "C" void fa_debug_set_split_pairs(int mode) {
     knobs_mut().split_pairs = mode < 0 ? env_defaults().split_pairs : mode;
+}
+// split-KV decode merge knob (Knobs::dec_fuse, env FA_DEC_FUSE): 1 (default) the last split of a unit
+// merges the partials in the decode kernel, 0 the separate fa_decode_combine launch; < 0 restores
+extern "C" void fa_debug_set_dec_fuse(int mode) {
+    knobs_mut().dec_fuse = mode < 0 ? env_defaults().dec_fuse : mode;
 }
 // zigzag knob (fa_launch.h Knobs::zigzag): 0 never, 1 when the blocks fit one round, 2 always; < 0
 // restores the environment / default value. fa_debug_last_zigzag: the causal block layout of the

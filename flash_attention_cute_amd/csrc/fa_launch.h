@@ -49,6 +49,7 @@ struct Knobs {
     int zigzag;
     int split;  // key-split causal Q blocks (use_split): 0 never, 1 where measured faster (default), 2 always
     int split_pairs;  // key-split pairs (use_split_pairs): 0 never, 1 where they fit one pass (default)
+    int dec_fuse;     // split-KV decode: 1 the last split of a unit merges (default), 0 fa_decode_combine
 };
 
 const Knobs &knobs();
@@ -152,6 +153,9 @@ inline int64_t split_wave_floats(int64_t headdim) {
 #ifndef FA_SPLIT_PAIRS
 #define FA_SPLIT_PAIRS 1
 #endif
+#ifndef FA_DEC_FUSE  // default of Knobs::dec_fuse
+#define FA_DEC_FUSE 1
+#endif
 // workgroups of a key-split launch over `units` plain blocks (2 pieces each) or pairs: every XCD gets
 // two workgroups per unit of its list when that fits the grid cap (units are dealt to XCDs, so 2 *
 // units workgroups could leave some XCD short and run both pieces of a block on one workgroup)
@@ -205,6 +209,11 @@ struct DecArgs {
     // per-sequence key positions [k_lo[b], k_hi[b]) within batch row b (a padded batch), or nullptr
     // (every key). Query ranges are not supported here (the dispatcher sends them to fa_fwd_w4).
     const int *k_lo, *k_hi;
+    // (n_split > 1) per-unit arrival counters, zero at the launch (the stream's persistent
+    // split_sync_area): the last split of a unit to finish merges the partials itself -- the unit's
+    // splits then run on ONE XCD (fa_decode "fused merge") -- and re-zeroes its counter; nullptr: the
+    // separate fa_decode_combine launch merges them
+    unsigned *cnt;
 };
 constexpr int kDecNt = 1;  // K/V LDS-DMA with the non-temporal cache policy
 

@@ -121,6 +121,42 @@ def test_decode_matches_prefill_kernel(fa, device):
     assert (a.float() - b.float()).abs().max().item() <= 1.6e-2
 
 
+FUSE = [  # (B, Hq, Hkv, Sq, Sk, D): split-KV launches (n_split > 1)
+    (1, 32, 8, 1, 16384, 128),   # decode_long's class: 8 units, one per XCD
+    (1, 12, 3, 1, 9000, 128),    # 3 units: XCDs 3..7 get none (their padded workgroups leave)
+    (2, 64, 1, 1, 5000, 64),     # MQA with 64 q-heads: two row blocks per (batch, kv-head)
+    (1, 8, 2, 3, 7000, 128),     # 3 query positions per q-head (unpacked rows)
+]
+
+
+@pytest.mark.parametrize("shape", FUSE, ids=lambda s: "x".join(map(str, s)))
+def test_decode_fused_merge(fa, device, shape):
+    """The last split of a (batch, kv-head, row block) merges the partials inside fa_decode (a.cnt:
+    the unit's splits on one XCD, the stream's persistent zeroed counters): bit-identical to the
+    separate fa_decode_combine launch at D = 128 (one output ulp at D = 64), against the oracle, and
+    twice in a row (the counters are left zero)."""
+    from flash_attention_cute_amd import _debug
+
+    b, hq, hkv, sq, sk, d = shape
+    q, k, v = (t.to(device) for t in make(b, hq, hkv, sq, sk, d, torch.float16, zlib.crc32(repr(shape).encode())))
+    try:
+        fused = fa(q, k, v)
+        assert _debug.last_path() == "decode_split"
+        again = fa(q, k, v)
+        _debug.set_dec_fuse(0)
+        sep = fa(q, k, v)
+        assert _debug.last_path() == "decode_split"
+    finally:
+        _debug.set_dec_fuse()
+    assert torch.equal(fused, again)
+    if d == 128:
+        assert torch.equal(fused, sep)
+    else:  # (hipcc folds fa_decode_combine's D = 64 O * 1/l into the f16 conversion, v_fma_mix: one
+        # rounding instead of two -- at most one output ulp apart)
+        assert (fused.float() - sep.float()).abs().max().item() <= 2 ** -10
+    check(fused.cpu(), q.cpu(), k.cpu(), v.cpu(), d ** -0.5, False, torch.float16)
+
+
 def test_decode_deterministic(fa, device):
     q, k, v = (t.to(device) for t in make(1, 32, 8, 1, 9000, 128, torch.float16, 4))
     assert torch.equal(fa(q, k, v), fa(q, k, v))
