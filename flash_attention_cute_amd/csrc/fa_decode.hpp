@@ -111,7 +111,9 @@ __device__ __forceinline__ void decode_merge(const fa_fwd_params &p, const DecAr
     }
 }
 
-template <class DT, bool kCausal, int kD, bool kExactD>
+// kFuse: the fused-merge body (a.cnt set; split launches only) -- a separate instantiation, so the
+// unsplit launches keep the kernel without the merge code
+template <class DT, bool kCausal, int kD, bool kExactD, bool kFuse = false>
 __global__ __launch_bounds__(256, 1) void fa_decode(const fa_fwd_params p, const DecArgs a) {
     using G = Geo<kD>;
     using DG = DecGeo<kD>;
@@ -135,7 +137,7 @@ __global__ __launch_bounds__(256, 1) void fa_decode(const fa_fwd_params p, const
     // (the hardware deals workgroups to XCDs by id mod 8), so the last one reads the others' partials
     // through its own L2; the grid pads every XCD to the same count (the extra workgroups leave)
     int split, unit;
-    if (a.cnt) {
+    if constexpr (kFuse) {
         const int k = (int)(blockIdx.x >> 3);
         unit = ((k / a.n_split) << 3) | (int)(blockIdx.x & 7);
         split = k % a.n_split;
@@ -404,7 +406,7 @@ __global__ __launch_bounds__(256, 1) void fa_decode(const fa_fwd_params p, const
                 *(float4 *)(dst + i) = make_float4(acc[i] * inv, acc[i + 1] * inv, acc[i + 2] * inv, acc[i + 3] * inv);
             if (part == 0) a.ws_lse[slot] = L > 0.f ? M + __builtin_amdgcn_logf(L) : kNeg;  // log2
         }
-        if (a.cnt) {
+        if constexpr (kFuse) {
             // fused merge: every thread's partials are in L2 before the workgroup arrives; the last
             // arrival merges the unit (the others' stores were drained before their arrivals, and
             // its loads bypass its CU's L1)
@@ -487,7 +489,10 @@ int launch_decode(const fa_fwd_params &p, DecArgs a, void *ws, hipStream_t strea
     }
     // (fused: every XCD holds ceil(units / 8) units' splits)
     const int64_t grid = a.cnt ? 8 * ((units + 7) / 8) * a.n_split : units * a.n_split;
-    hipLaunchKernelGGL((fa_decode<DT, C, kD, kExact>), dim3((uint32_t)grid), dim3(256), 0, stream, p, a);
+    if (a.cnt)
+        hipLaunchKernelGGL((fa_decode<DT, C, kD, kExact, true>), dim3((uint32_t)grid), dim3(256), 0, stream, p, a);
+    else
+        hipLaunchKernelGGL((fa_decode<DT, C, kD, kExact>), dim3((uint32_t)grid), dim3(256), 0, stream, p, a);
     if (a.n_split > 1 && !a.cnt)
         hipLaunchKernelGGL((fa_decode_combine<DT, kD, kExact>),
                            dim3((uint32_t)(p.batch_size * p.num_heads_kv * ((a.rows + 3) / 4))), dim3(256), 0, stream,
