@@ -40,6 +40,7 @@ import json
 import os
 import platform
 import statistics
+import struct
 import sys
 import time
 from pathlib import Path
@@ -111,12 +112,67 @@ def algo_bytes(c) -> int:
     return (2 * c["B"] * c["Hq"] * c["Sq"] * c["D"] + 2 * c["B"] * c["Hkv"] * c["Sk"] * c["D"]) * 2
 
 
-def lib_sha16() -> str:
+def _lib_path(path=None) -> Path:
+    return Path(path) if path else ROOT / "flash_attention_cute_amd" / "lib" / "libfa_gfx950.so"
+
+
+def lib_sha16(path=None) -> str:
     """First 16 hex digits of the sha256 of the C-ABI library in the tree (the one the op loads)."""
     import hashlib
 
-    p = ROOT / "flash_attention_cute_amd" / "lib" / "libfa_gfx950.so"
+    p = _lib_path(path)
     return hashlib.sha256(p.read_bytes()).hexdigest()[:16] if p.exists() else "missing"
+
+
+def _elf_sections(blob: bytes) -> dict:
+    """{name: [(offset, size)]} of an ELF64 little-endian image (section headers only)."""
+    shoff, = struct.unpack_from("<Q", blob, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", blob, 0x3A)
+    hdrs = [struct.unpack_from("<IIQQQQ", blob, shoff + i * shentsize) for i in range(shnum)]
+    stro = hdrs[shstrndx][4]
+    out = {}
+    for h in hdrs:
+        name = blob[stro + h[0]: blob.index(b"\0", stro + h[0])].decode()
+        out.setdefault(name, []).append((h[4], h[5]))
+    return out
+
+
+def code_sha16(path=None) -> str:
+    """First 16 hex digits of a sha256 over the gfx950 DEVICE code of the library: the ``.text`` and
+    ``.rodata`` (kernel descriptors) of every amdgcn code object in its ``.hip_fatbin`` offload bundles,
+    one digest per object, sorted. Host code, symbol tables and the per-compile unique ids hipcc puts in
+    each object are left out, so a rebuild of identical source keeps the value (the whole-file
+    ``lib_sha16`` changes with every build)."""
+    import hashlib
+
+    p = _lib_path(path)
+    if not p.exists():
+        return "missing"
+    blob = p.read_bytes()
+    secs = _elf_sections(blob).get(".hip_fatbin")
+    if not secs:
+        return "no-device-code"
+    off, size = secs[0]
+    fat = blob[off: off + size]
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    digests, pos = [], 0
+    while (i := fat.find(magic, pos)) >= 0:
+        n, = struct.unpack_from("<Q", fat, i + 24)
+        q = i + 32
+        for _ in range(n):
+            eoff, esize, tl = struct.unpack_from("<QQQ", fat, q)
+            triple = fat[q + 24: q + 24 + tl].decode()
+            q += 24 + tl
+            if "amdgcn" in triple and esize:
+                co = fat[i + eoff: i + eoff + esize]
+                cs = _elf_sections(co)
+                h = hashlib.sha256()
+                for name in (".text", ".rodata"):
+                    for so, ss in cs.get(name, []):
+                        h.update(co[so: so + ss])
+                digests.append(h.hexdigest())
+        pos = q
+    return hashlib.sha256("".join(sorted(digests)).encode()).hexdigest()[:16]
 
 
 def cpu_model() -> str:
@@ -309,7 +365,8 @@ def strong_calls(c, q, k, v, runs, dense_fn, window_fn, padded_fn):
 
 def load_traffic(config_key: str):
     """(HBM bytes per launch, provenance) from profiles/pmc_<config>.json -- only when that PMC pass
-    profiled THIS library (its ``lib_sha16`` equals the loaded library's); otherwise (None, why)."""
+    profiled THIS library's device code (its ``code_sha16`` equals the loaded library's: a rebuild of
+    the same source keeps it); otherwise (None, why)."""
     p = ROOT / "profiles" / f"pmc_{config_key}.json"
     if not p.exists():
         return None, {"traffic_source": None}
@@ -317,7 +374,7 @@ def load_traffic(config_key: str):
         d = json.loads(p.read_text())
     except Exception:  # noqa: BLE001
         return None, {"traffic_source": None}
-    prof, cur = d.get("lib_sha16"), lib_sha16()
+    prof, cur = d.get("code_sha16"), code_sha16()
     if prof != cur:
         return None, {"traffic_stale": True, "traffic_profiled_lib": prof, "traffic_this_lib": cur,
                       "traffic_of_profiled_lib": d.get("hbm_bytes_per_launch")}

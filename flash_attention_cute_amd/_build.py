@@ -111,9 +111,12 @@ def build_abi(force: bool = False, verbose: bool = False, stamps: bool = False, 
         # builds compile what the product does, so an A/B against the product library compares like code)
         extra = ["-DFA_DEBUG_VARIANTS=1"] + extra
     objdir.mkdir(parents=True, exist_ok=True)
-    cmds = []
+    cmds = []  # (command, object, inputs): an object newer than its inputs, built by the same command, is kept
     objs = []
     asm_files = []
+    tooling = [Path(__file__).resolve()]
+    headers = [CSRC / "fa_launch.h", *sorted(INCLUDE.glob("*.h"))]
+    inst_deps = [p for ext in ("*.hpp", "*.h", "*.inc") for p in sorted(CSRC.glob(ext))] + [CSRC / "fa_inst.hip"]
     for dt, c, d, e in INSTANCES:
         # one directory per instantiation: -save-temps=obj names its files after the source
         idir = objdir / f"{dt.lower()}_c{c}_d{d}_x{e}"
@@ -123,15 +126,26 @@ def build_abi(force: bool = False, verbose: bool = False, stamps: bool = False, 
         stub = ["-DFA_INST_STUB=1"] if only and (dt, c, d, e) not in only else []
         if not stub:
             asm_files.append(idir / f"fa_inst-hip-amdgcn-amd-amdhsa-{ARCH}.s")
-        cmds.append([HIPCC, *HIP_FLAGS, *extra, *stub, f"-I{INCLUDE}", f"-I{CSRC}", f"-DFA_INST_DT={dt}",
-                     f"-DFA_INST_CAUSAL={c}", f"-DFA_INST_D={d}", f"-DFA_INST_EXACT={e}", "-save-temps=obj",
-                     "-Wno-inline-asm", "-c", CSRC / "fa_inst.hip", "-o", obj])
+        cmds.append(([HIPCC, *HIP_FLAGS, *extra, *stub, f"-I{INCLUDE}", f"-I{CSRC}", f"-DFA_INST_DT={dt}",
+                      f"-DFA_INST_CAUSAL={c}", f"-DFA_INST_D={d}", f"-DFA_INST_EXACT={e}", "-save-temps=obj",
+                      "-Wno-inline-asm", "-c", CSRC / "fa_inst.hip", "-o", obj], obj, inst_deps + tooling))
     for src in ("fa_fwd_gfx950.hip", "fa_rope.hip"):  # C-ABI dispatcher, standalone RoPE kernel
         obj = objdir / src.replace(".hip", ".o")
         objs.append(obj)
-        cmds.append([HIPCC, *HIP_FLAGS, *extra, f"-I{INCLUDE}", f"-I{CSRC}", "-c", CSRC / src, "-o", obj])
+        cmds.append(([HIPCC, *HIP_FLAGS, *extra, f"-I{INCLUDE}", f"-I{CSRC}", "-c", CSRC / src, "-o", obj], obj,
+                     [CSRC / src, *headers, *tooling]))
+
+    def compile_one(cmd, obj, deps):
+        stamp = obj.with_suffix(".cmd")
+        line = " ".join(map(str, cmd))
+        if (not force and not _stale(obj, deps) and stamp.exists() and stamp.read_text() == line
+                and (obj.name != "fa_inst.o" or next(obj.parent.glob("*.s"), None) is not None)):
+            return
+        _run(cmd, verbose)
+        stamp.write_text(line)
+
     with ThreadPoolExecutor(max_workers=_jobs()) as ex:
-        for f in [ex.submit(_run, cmd, verbose) for cmd in cmds]:
+        for f in [ex.submit(compile_one, *c) for c in cmds]:
             f.result()
     # gate: the literal-AGPR invariant of fa_fwd_w4 and no VGPR spills (_asm_check)
     from ._asm_check import check_file

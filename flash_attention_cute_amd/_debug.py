@@ -61,6 +61,14 @@ def lib(debug: bool = False) -> ctypes.CDLL:
         lib.fa_debug_last_zigzag.restype = ctypes.c_int
         lib.fa_split_errors.argtypes = [ctypes.c_int]
         lib.fa_split_errors.restype = ctypes.c_int64
+        lib.fa_debug_set_xccs.argtypes = [ctypes.c_int]
+        lib.fa_debug_set_xccs.restype = None
+        lib.fa_debug_set_split_fault.argtypes = [ctypes.c_int]
+        lib.fa_debug_set_split_fault.restype = None
+        lib.fa_debug_last_dec_fused.restype = ctypes.c_int
+        lib.fa_fwd_gfx950_workspace_size.restype = ctypes.c_int64
+        lib.fa_fwd_gfx950_ws.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
+                                         ctypes.c_void_p]
         _libs[debug] = lib
     return _libs[debug]
 
@@ -123,6 +131,22 @@ def set_dec_fuse(mode: int | None = None, debug: bool = False) -> None:
     lib(debug).fa_debug_set_dec_fuse(-1 if mode is None else int(mode))
 
 
+def set_xccs(n: int | None = None, debug: bool = False) -> None:
+    """XCDs per device seen by the placement check (fa_launch.h same_xcd_placement: key-split and the
+    fused decode merge need the count to divide 8); None restores the device's own count."""
+    lib(debug).fa_debug_set_xccs(-1 if n is None else int(n))
+
+
+def set_split_fault(on: bool) -> None:
+    """DEBUG library only: force one key-split hand-off per launch (slot 0, wave 0) to time out."""
+    lib(debug=True).fa_debug_set_split_fault(1 if on else 0)
+
+
+def last_dec_fused(debug: bool = False) -> bool:
+    """Whether the last split-KV decode launch on this thread merged its partials in-kernel."""
+    return lib(debug).fa_debug_last_dec_fused() == 1
+
+
 def last_layout(debug: bool = False) -> str:
     """Causal block layout of the last prefill launch on this thread: "plain", "zigzag" or "split"
     (key-split, as halves or as pairs: last_split_pairs)."""
@@ -134,10 +158,12 @@ def last_split_pairs(debug: bool = False) -> bool:
     return lib(debug).fa_debug_last_zigzag() == 3
 
 
-def forward(q, k, v, softmax_scale=None, causal=False, variant="w8", window_left=-1, w4_grid=None):
+def forward(q, k, v, softmax_scale=None, causal=False, variant="w8", window_left=-1, w4_grid=None,
+            workspace=False):
     """Attention through a kernel body of the DEBUG library (tests: the parity sweep over w8 / w4slow /
     p8): the op's host steps (reference flash_attention/flash_attention.py:17-53 and
-    csrc/flash_attention_api.cpp:64-133, restated) over lib/libfa_gfx950_debug.so's C-ABI."""
+    csrc/flash_attention_api.cpp:64-133, restated) over lib/libfa_gfx950_debug.so's C-ABI;
+    ``workspace``: through fa_fwd_gfx950_ws with the workspace it asks for, as the op does."""
     import torch
 
     dl = lib(debug=True)
@@ -165,6 +191,10 @@ def forward(q, k, v, softmax_scale=None, causal=False, variant="w8", window_left
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     if window_left >= 0:
         rc = dl.fa_fwd_gfx950_window(ctypes.byref(p), dtype, int(causal), ctypes.c_int64(window_left), stream)
+    elif workspace:
+        need = dl.fa_fwd_gfx950_workspace_size(ctypes.byref(p), dtype, int(causal))
+        ws = torch.empty(max(need, 16), dtype=torch.uint8, device=q.device)
+        rc = dl.fa_fwd_gfx950_ws(ctypes.byref(p), dtype, int(causal), ws.data_ptr(), need, stream)
     else:
         rc = dl.fa_fwd_gfx950(ctypes.byref(p), dtype, int(causal), stream)
     if rc != 0:

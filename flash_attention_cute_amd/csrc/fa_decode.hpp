@@ -483,10 +483,13 @@ int launch_decode(const fa_fwd_params &p, DecArgs a, void *ws, hipStream_t strea
         a.ws_o = (float *)ws;
         a.ws_lse = (float *)((char *)ws + slots * kD * 4);
     }
-    if (a.n_split > 1 && knobs().dec_fuse) {  // fused merge: the stream's zeroed per-unit counters, if any
+    // fused merge: the stream's zeroed per-unit counters (none under graph capture), and only where a
+    // unit's splits share an XCD (same_xcd_placement)
+    if (a.n_split > 1 && knobs().dec_fuse && same_xcd_placement()) {
         unsigned *err = nullptr;
         a.cnt = split_sync_area(stream, units * 4, &err);
     }
+    set_last_dec_fused(a.cnt != nullptr);
     // (fused: every XCD holds ceil(units / 8) units' splits)
     const int64_t grid = a.cnt ? 8 * ((units + 7) / 8) * a.n_split : units * a.n_split;
     if (a.cnt)

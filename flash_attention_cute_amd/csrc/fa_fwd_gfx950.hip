@@ -37,7 +37,7 @@ unsigned long long *g_stamps = nullptr;
 thread_local int g_last_path = fa::kPathNone;
 
 fa::Knobs knobs_from_env() {
-    fa::Knobs k{0, 0, 1, fa::kDecTargetWgs, fa::kDecNt, 1, 1, FA_SPLIT_PAIRS, FA_DEC_FUSE};
+    fa::Knobs k{0, 0, 1, fa::kDecTargetWgs, fa::kDecNt, 1, 1, FA_SPLIT_PAIRS, FA_DEC_FUSE, 0, 0};
     if (const char *v = getenv("FA_GFX950_VARIANT"))
         k.variant = !strcmp(v, "w8") ? 1 : !strcmp(v, "w4slow") ? 2 : !strcmp(v, "p8") ? 3 : 0;
     if (const char *e = getenv("FA_W4_GRID")) k.w4_grid = atoll(e) > 0 ? atoll(e) : 0;
@@ -48,6 +48,7 @@ fa::Knobs knobs_from_env() {
     if (const char *e = getenv("FA_SPLIT")) k.split = atoi(e);
     if (const char *e = getenv("FA_SPLIT_PAIRS")) k.split_pairs = atoi(e);
     if (const char *e = getenv("FA_DEC_FUSE")) k.dec_fuse = atoi(e);
+    if (const char *e = getenv("FA_XCCS")) k.xccs = atoi(e) > 0 ? atoi(e) : 0;
 #ifdef FA_DEBUG_VARIANTS
     if (k.variant != 0)  // a debug / A-B body replaces the product kernel for the whole process: say so
         fprintf(stderr,
@@ -113,6 +114,18 @@ extern "C" void fa_debug_set_split_pairs(int mode) {
 extern "C" void fa_debug_set_dec_fuse(int mode) {
     knobs_mut().dec_fuse = mode < 0 ? env_defaults().dec_fuse : mode;
 }
+// placement knob (Knobs::xccs, env FA_XCCS): XCDs per device for same_xcd_placement (0 / < 0: the
+// device's own count) -- tests force a count that does not divide 8 to see the fallback layouts
+extern "C" void fa_debug_set_xccs(int n) { knobs_mut().xccs = n < 0 ? env_defaults().xccs : n; }
+// (debug library only) force one key-split hand-off per launch to time out (slot 0, wave 0; fa_fwd_w4
+// dbg & 2): 1 on, 0 off; the product library ignores it
+extern "C" void fa_debug_set_split_fault(int on) {
+#ifdef FA_DEBUG_VARIANTS
+    knobs_mut().split_fault = on > 0 ? 1 : 0;
+#else
+    (void)on;
+#endif
+}
 // zigzag knob (fa_launch.h Knobs::zigzag): 0 never, 1 when the blocks fit one round, 2 always; < 0
 // restores the environment / default value. fa_debug_last_zigzag: the causal block layout of the
 // last prefill launch on this thread: 0 plain, 1 zigzag, 2 key-split, 3 key-split pairs.
@@ -149,24 +162,46 @@ int64_t fa::w4_grid_split(int64_t units) {
     return n < cap ? n : cap;
 }
 
-// Key-split counter areas (fa_launch.h split_sync_area): one per (device, stream), allocated and zeroed
-// the first time a key-split launch runs on that stream outside graph capture, never freed (a captured
-// graph keeps using the area its launches were given). The kernel's combining pieces zero their counters
-// again, so the area is zero between launches and no launch needs a memset. Streams of one device that
-// run key-split launches concurrently each get their own area.
+int64_t fa::device_xccs() {
+    if (fa::knobs().xccs > 0) return fa::knobs().xccs;
+    // XCDs per device, queried once (a racing first query writes the same value); unknown -> 0, which
+    // fails same_xcd_placement (the dispatcher then takes the layouts without a hand-off)
+    static int xccs[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    if (xccs[dev] <= 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeNumberOfXccs, dev) != hipSuccess || n <= 0) return 0;
+        xccs[dev] = n;
+    }
+    return xccs[dev];
+}
+
+// Key-split / fused-decode counter areas (fa_launch.h split_sync_area): one per (device, stream),
+// allocated the first time such an eager launch runs on that stream and zeroed by a memset ON THAT
+// STREAM (ordered before the launch that gets it; no hipDeviceSynchronize, which would stall every
+// stream of the device and break another thread's graph capture), never freed. The kernels zero their
+// counters again -- a timed-out key-split hand-off included (fa_fwd_w4 abandons the pair) -- so the
+// area is zero between launches and no launch needs a memset. Each area ends in its stream's hand-off
+// error counter. Launches under graph capture never get an area (split_sync_area).
 namespace {
 constexpr int64_t kSyncAreaBytes = 256 * 1024;  // 8192 blocks x 4 waves x 2 counters
+constexpr int64_t kAreaAlloc = kSyncAreaBytes + 256;  // + the error counter
 constexpr int kMaxAreas = 64;
 struct SyncArea {
     int dev;
     hipStream_t stream;
     unsigned *ptr;
+    unsigned *err() const { return ptr + kSyncAreaBytes / 4; }
 };
 std::mutex g_sync_mu;
 SyncArea g_areas[kMaxAreas];
 int g_n_areas = 0;
-unsigned *g_split_err[64] = {};  // per device: hand-offs that timed out
+thread_local int g_last_dec_fused = 0;
 }  // namespace
+
+void fa::set_last_dec_fused(bool fused) { g_last_dec_fused = fused ? 1 : 0; }
+extern "C" int fa_debug_last_dec_fused(void) { return g_last_dec_fused; }
 
 unsigned *fa::split_sync_area(hipStream_t stream, int64_t bytes, unsigned **err) {
     *err = nullptr;
@@ -176,42 +211,54 @@ unsigned *fa::split_sync_area(hipStream_t stream, int64_t bytes, unsigned **err)
     if (hipStreamIsCapturing(stream, &cs) != hipSuccess) return nullptr;
     const bool capturing = cs != hipStreamCaptureStatusNone;
     std::lock_guard<std::mutex> lk(g_sync_mu);
-    if (!g_split_err[dev] && !capturing) {  // (synchronous: ordered before every stream's later launches)
-        unsigned *e = nullptr;
-        if (hipMalloc(&e, 256) == hipSuccess) {
-            if (hipMemset(e, 0, 256) == hipSuccess && hipDeviceSynchronize() == hipSuccess) g_split_err[dev] = e;
-            else (void)hipFree(e);
-        }
-    }
-    *err = g_split_err[dev];
-    if (bytes > kSyncAreaBytes) return nullptr;
-    for (int i = 0; i < g_n_areas; ++i)
-        if (g_areas[i].dev == dev && g_areas[i].stream == stream) return g_areas[i].ptr;
-    if (capturing || g_n_areas >= kMaxAreas) return nullptr;
-    unsigned *a = nullptr;
-    if (hipMalloc(&a, kSyncAreaBytes) != hipSuccess) return nullptr;
-    if (hipMemset(a, 0, kSyncAreaBytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-        (void)hipFree(a);
+    SyncArea *a = nullptr;
+    for (int i = 0; i < g_n_areas && !a; ++i)
+        if (g_areas[i].dev == dev && g_areas[i].stream == stream) a = &g_areas[i];
+    if (capturing) {  // (a graph's replays may run beside eager launches on this stream: no shared counters)
+        *err = a ? a->err() : nullptr;
         return nullptr;
     }
-    g_areas[g_n_areas++] = {dev, stream, a};
-    return a;
+    if (!a) {
+        if (g_n_areas >= kMaxAreas) return nullptr;
+        unsigned *ptr = nullptr;
+        // (this thread in relaxed capture mode for the allocation: another stream of the process may be
+        // capturing a graph in global mode, which forbids hipMalloc to threads in global mode -- the
+        // allocation is not part of any capture, and this stream is not capturing)
+        hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+        const bool swapped = hipThreadExchangeStreamCaptureMode(&mode) == hipSuccess;
+        const hipError_t me = hipMalloc(&ptr, kAreaAlloc);
+        if (swapped) (void)hipThreadExchangeStreamCaptureMode(&mode);
+        if (me != hipSuccess) return nullptr;
+        if (hipMemsetAsync(ptr, 0, kAreaAlloc, stream) != hipSuccess) {
+            (void)hipFree(ptr);
+            return nullptr;
+        }
+        g_areas[g_n_areas] = {dev, stream, ptr};
+        a = &g_areas[g_n_areas++];
+    }
+    *err = a->err();
+    return bytes > kSyncAreaBytes ? nullptr : a->ptr;
 }
 
 extern "C" int64_t fa_split_errors(int reset) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-    unsigned *e = nullptr;
+    unsigned *errs[kMaxAreas];
+    int n_err = 0;
     {
         std::lock_guard<std::mutex> lk(g_sync_mu);
-        e = g_split_err[dev];
+        for (int i = 0; i < g_n_areas; ++i)
+            if (g_areas[i].dev == dev) errs[n_err++] = g_areas[i].err();
     }
-    if (!e) return 0;
-    unsigned n = 0;
-    if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(&n, e, sizeof(n), hipMemcpyDeviceToHost) != hipSuccess)
-        return 0;
-    if (reset && n) (void)hipMemset(e, 0, sizeof(unsigned));
-    return (int64_t)n;
+    if (!n_err || hipDeviceSynchronize() != hipSuccess) return 0;
+    int64_t total = 0;
+    for (int i = 0; i < n_err; ++i) {
+        unsigned n = 0;
+        if (hipMemcpy(&n, errs[i], sizeof(n), hipMemcpyDeviceToHost) != hipSuccess) return total;
+        total += n;
+        if (reset && n) (void)hipMemset(errs[i], 0, sizeof(unsigned));
+    }
+    return total;
 }
 
 int64_t fa::w4_grid(int64_t nwg) {

@@ -2278,14 +2278,27 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         // unnormalised O (AGPR fragment order, 64 lanes x 16 B per record) and its (nmsc, l, m) per
         // lane in the workspace and marks them ready in the arrivals word; the second finds them
         // ready in its own arrival, or waits for the mark (the first has finished its tiles and only
-        // stores), rescales both to their larger reference and stores O. (The pieces run on one XCD
-        // by work_of's order; the accesses do not rely on it.)
+        // stores), rescales both to their larger reference and stores O. The hand-off RELIES on both
+        // pieces running on one XCD (work_of's order + the host's placement check, fa_launch.h
+        // same_xcd_placement): its sc1 accesses meet in that XCD's L2 (see st_ws).
         constexpr int kWaveF = 64 * (32 * DTL + kSplitStatsPerLane);
         unsigned *sync = xa.split_sync + 2 * ((size_t)slot_c * 4 + wave);
         u32x4 *wsw = (u32x4 *)(xa.split_ws + ((size_t)slot_c * 4 + wave) * kWaveF);
         u32x4 *stats = wsw + 8 * DTL * 64;  // after the 2 x DTL x 4 O records
-        // sync[0]: arrivals + kReady once the first piece's records are written (sync[1] is unused)
+        // sync[0]: arrivals + kReady once the first piece's records are written (sync[1] is unused).
+        // Within a launch the word runs 0 -> 1 -> 2 (arrivals) with + kReady at any point after 1, and
+        // the combining piece zeroes it, so every launch finds it 0. A second piece whose poll times out
+        // ABANDONS the pair: it swaps 2 (both arrived, not ready) for 0, so the first piece's late
+        // + kReady reads 0 and takes its own add back -- no launch inherits a stale ready mark.
         constexpr uint32_t kReady = 4;
+#ifdef FA_DEBUG_VARIANTS
+        // (debug library, dbg & 2: force one hand-off to time out -- wave 0 of the last q-tile of
+        // (batch 0, q-head 0), split in both layouts: the first piece holds its ready mark until its
+        // partner has abandoned the pair, the partner polls briefly)
+        const bool fault = (dbg & 2) && slot_c == nqp - 1 && wave == 0;
+#else
+        constexpr bool fault = false;
+#endif
         uint32_t arrived = 0;
         if (lane == 0) arrived = __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         arrived = __builtin_amdgcn_readfirstlane(arrived);
@@ -2303,24 +2316,41 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
                                         __float_as_uint(st[0].l), __float_as_uint(st[1].l)});
             st_ws(stats + 64 + lane, (u32x4){__float_as_uint(st[0].m), __float_as_uint(st[1].m), 0u, 0u});
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (every lane's records written through before the flag)
-            // ready: + kReady on the arrivals word (an add: the partner's arrival may land in between)
-            if (lane == 0) __hip_atomic_fetch_add(sync, kReady, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) {
+                if (fault)  // (debug: until the partner has arrived and abandoned the pair, bounded)
+                    for (int it = 0; it < (1 << 22); ++it) {
+                        __builtin_amdgcn_s_sleep(8);
+                        if (it > 64 && __hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) break;
+                    }
+                // ready: + kReady on the arrivals word (an add: the partner's arrival may land in between).
+                // It reads 0 only if the partner abandoned the pair: then no one else touches the word in
+                // this launch, and the add is taken back for the next one
+                if (__hip_atomic_fetch_add(sync, kReady, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+                    __hip_atomic_store(sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             split_role = 1;
         } else {
             split_role = 3;
             // the arrival already saw the records ready (the pairs layout's usual case: the partner
             // finished long before), or a bounded poll (~1 s), so a protocol failure never hangs the
-            // GPU; a timeout is counted in the device's error counter (fa_split_errors) -- the rows it
-            // combines are wrong
+            // GPU; a timeout abandons the pair (2 -> 0, above) and is counted in the stream's error
+            // counter (fa_split_errors) -- the rows it combines are wrong
             if (lane == 0) {
                 bool seen = arrived >= kReady;
-                for (int it = 0; !seen && it < (1 << 22); ++it) {
+                const int polls = fault ? 64 : (1 << 22);
+                for (int it = 0; !seen && it < polls; ++it) {
                     __builtin_amdgcn_s_sleep(8);
                     seen = __hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= kReady;
                 }
-                if (!seen && xa.split_err) __hip_atomic_fetch_add(xa.split_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (!seen) {
+                    unsigned expect = 2u;  // (the ready mark may land now: then the records are there)
+                    seen = !__hip_atomic_compare_exchange_strong(sync, &expect, 0u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT);
+                    if (!seen && xa.split_err)
+                        __hip_atomic_fetch_add(xa.split_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
                 // both pieces are past their last access to the pair: zero it for the next launch
-                __hip_atomic_store(sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (seen) __hip_atomic_store(sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: loads stay below the poll)
 #if FA_SPLIT_AGPR && FA_QLDS != 2  // (staging 2 may have read the next block's Q into those AGPRs already)
@@ -2446,7 +2476,7 @@ int launch_one(const fa_fwd_params &p, const PathArgs &xa, hipStream_t stream) {
         hipLaunchKernelGGL((fa_fwd_w4<DT, C, kD, kExact>),
                            dim3((uint32_t)(xz.split_ws ? w4_grid_split(xz.split_pairs ? n_pairs : nwg / 2) : w4_grid(nwg))),
                            dim3(256), 0, stream, p,
-                           (int)n_qtiles, variant == 2 ? 1 : 0, stamp_buffer(), xz);
+                           (int)n_qtiles, (variant == 2 ? 1 : 0) | (knobs().split_fault ? 2 : 0), stamp_buffer(), xz);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "HIP launch failed: %s", hipGetErrorString(e));
     set_last_path(variant == 1 ? kPathW8 : variant == 2 ? kPathW4Slow : kPathW4);

@@ -50,6 +50,8 @@ struct Knobs {
     int split;  // key-split causal Q blocks (use_split): 0 never, 1 where measured faster (default), 2 always
     int split_pairs;  // key-split pairs (use_split_pairs): 0 never, 1 where they fit one pass (default)
     int dec_fuse;     // split-KV decode: 1 the last split of a unit merges (default), 0 fa_decode_combine
+    int xccs;         // XCDs per device for the placement check (0: the device's own count; tests)
+    int split_fault;  // (debug library only) force one key-split hand-off to time out (kernel dbg & 2)
 };
 
 const Knobs &knobs();
@@ -59,6 +61,7 @@ inline int variant_from_env() { return knobs().variant; }
 enum Path { kPathNone = 0, kPathW4 = 1, kPathW8 = 2, kPathW4Slow = 3, kPathDecode = 4, kPathDecodeSplit = 5, kPathP8 = 6 };
 void set_last_path(int path);
 void set_last_zigzag(int z);
+void set_last_dec_fused(bool fused);  // (fa_debug_last_dec_fused: the last decode launch merged in-kernel)
 
 // diagnostic per-wave phase stamps of fa_fwd_w4 (only a -DFA_STAMPS=1 build writes them; see
 // fa_debug_set_stamps in fa_fwd_gfx950.hip and scripts/stamps.py); nullptr otherwise
@@ -70,6 +73,18 @@ unsigned long long *stamp_buffer();
 int64_t w4_grid(int64_t nwg);
 // compute units of the current device (queried once per device)
 int64_t device_cus();
+// XCDs (XCCs) of the current device (queried once per device; the xccs knob overrides it)
+int64_t device_xccs();
+// Whether workgroups b and b + 8 of a launch share an XCD, the placement that the key-split hand-off
+// and the fused decode merge rely on (their sc1 records meet in that XCD's L2, no L2 write-back or
+// invalidate). The hardware deals a launch's workgroups to the XCDs round-robin by workgroup id
+// (MI355X_MICROARCH "Workgroup dispatch"), so this holds when the XCD count divides 8: 8 (SPX, 256
+// CUs), 4 (DPX), 2, 1 (CPX). Otherwise the dispatcher runs the layouts that need no hand-off (zigzag
+// prefill, the separate decode combine launch).
+inline bool same_xcd_placement() {
+    const int64_t x = device_xccs();
+    return x >= 1 && 8 % x == 0;
+}
 
 
 
@@ -137,6 +152,7 @@ inline int64_t zigzag_qtiles(int64_t seqlen_q) { return ((seqlen_q + 127) / 128 
 // wave) the partial O of its 64 rows (32 * DTL fp32 per lane) and two 16-byte statistic records per lane.
 inline bool use_split(const fa_fwd_params &p, bool causal, const PathArgs &xa) {
     if (!causal || xa.k_rng || xa.cos || xa.window_left >= 0 || knobs().split == 0 || p.seqlen_q <= 128) return false;
+    if (!same_xcd_placement()) return false;  // (the pieces' hand-off needs one XCD per pair)
     if (knobs().split == 2) return true;
     const int64_t nwg = (p.seqlen_q + kBlockM - 1) / kBlockM * p.num_heads_q * p.batch_size, cus = device_cus();
     return nwg <= cus && (p.seqlen_kv >= 3072 || (p.seqlen_kv >= 2048 && 2 * nwg <= cus));
@@ -173,10 +189,13 @@ inline int64_t split_ws_bytes(const fa_fwd_params &p) {
     return split_sync_bytes(p) + split_blocks(p) * 4 * split_wave_floats(p.headdim) * 4;
 }
 
-// The key-split counters of launches on `stream` of the current device: a device area allocated and
-// zeroed once (the kernel leaves it zeroed), or nullptr when `bytes` exceed it or the stream is capturing
-// a graph before the area exists (the caller then zeroes counters in its workspace). *err: the device's
-// hand-off error counter (nullptr under capture before it exists).
+// The key-split / fused-decode counters of eager launches on `stream` of the current device: a device
+// area allocated once per (device, stream) and zeroed by a memset on that stream (stream-ordered, no
+// device synchronisation; the kernels leave it zeroed), or nullptr when `bytes` exceed it or the stream
+// is capturing a graph -- a graph never holds the shared area (its replays could run beside eager
+// launches on the stream), the caller then zeroes counters in its workspace (a memset node) or runs the
+// separate decode combine. *err: the stream's hand-off error counter (under capture: the capturing
+// stream's, if it has an area; else nullptr).
 unsigned *split_sync_area(hipStream_t stream, int64_t bytes, unsigned **err);
 
 // launch one (dtype, causal, head-dim tile, exact head dim) instantiation on `stream`
@@ -211,8 +230,10 @@ struct DecArgs {
     const int *k_lo, *k_hi;
     // (n_split > 1) per-unit arrival counters, zero at the launch (the stream's persistent
     // split_sync_area): the last split of a unit to finish merges the partials itself -- the unit's
-    // splits then run on ONE XCD (fa_decode "fused merge") -- and re-zeroes its counter; nullptr: the
-    // separate fa_decode_combine launch merges them
+    // splits then run on ONE XCD (fa_decode "fused merge"; the partials are published by stores drained
+    // before a relaxed agent-scope add, with no release / acquire fence, which is enough ONLY inside one
+    // XCD's L2: the host checks same_xcd_placement) -- and re-zeroes its counter; nullptr: the separate
+    // fa_decode_combine launch merges them
     unsigned *cnt;
 };
 constexpr int kDecNt = 1;  // K/V LDS-DMA with the non-temporal cache policy

@@ -45,8 +45,13 @@ extern "C" {
 
 /* 7: fa_fwd_gfx950_ws takes the key-split layout only when the workspace is large enough (a smaller one
  *    runs the zigzag layout instead of failing), its counters live in a per-(device, stream) area the
- *    library keeps zeroed (no per-call memset), and fa_split_errors() reports failed hand-offs. */
-#define FA_GFX950_ABI_VERSION 7
+ *    library keeps zeroed (no per-call memset), and fa_split_errors() reports failed hand-offs.
+ * 8: the per-stream area is zeroed by a memset on the launching stream (no device-wide
+ *    synchronisation on a stream's first call), graph captures never use it (workspace counters), a
+ *    timed-out hand-off leaves it zeroed, the error count is kept per stream (fa_split_errors sums the
+ *    device's), and key-split / the fused decode merge run only where workgroups b and b + 8 share an
+ *    XCD (the XCD count divides 8). */
+#define FA_GFX950_ABI_VERSION 8
 
 /* Field order mirrors reference csrc/flash_attention.h:5-37. */
 typedef struct fa_fwd_params {
@@ -115,9 +120,13 @@ int fa_fwd_gfx950(const fa_fwd_params *params, int dtype, int causal, void *stre
  * fa_fwd_gfx950_workspace_size() bytes (else the blocks run unsplit, in zigzag
  * order); the workspace then holds the first piece's fp32 partial O. The pieces'
  * per-block counters live in a device area the library allocates once per
- * (device, stream) outside graph capture and the kernel leaves zeroed (under
- * capture with no area yet, the counters go to the workspace, zeroed by this
- * call on `stream`). With workspace == NULL it behaves exactly like
+ * (device, stream) on the first such eager call on that stream (hipMalloc, then
+ * a memset enqueued on `stream`: no device synchronisation) and the kernel
+ * leaves zeroed; under graph capture the counters go to the workspace instead,
+ * zeroed by a memset node this call adds on `stream`. The split layouts need
+ * workgroups b and b + 8 of a launch on one XCD (the device's XCD count divides
+ * 8, MI355X deals workgroups to XCDs round-robin); elsewhere the blocks run
+ * unsplit. With workspace == NULL it behaves exactly like
  * fa_fwd_gfx950 (decode kernel unsplit, causal prefill in zigzag blocks). The
  * workspace is scratch: it may be reused as soon as the launch completes in
  * stream order. 16-byte aligned.
@@ -142,7 +151,8 @@ int fa_fwd_gfx950_check(const fa_fwd_params *params, int dtype, int causal);
 /*
  * Key-split hand-offs on the current device that timed out (a piece whose partner's
  * partial result did not arrive within ~1 s combined what was there: its rows are
- * wrong), summed over launches since the last reset; 0 when none. Synchronises
+ * wrong; the pair is abandoned, so later launches are unaffected), summed over the
+ * device's streams and launches since the last reset; 0 when none. Synchronises
  * with the device. reset != 0 zeroes the count.
  */
 int64_t fa_split_errors(int reset);

@@ -26,10 +26,10 @@ if not agg:  # (a missing or empty profile directory must not overwrite a good p
     sys.exit(f"pmc_to_json: no counter rows of {KERNELS} under {src}")
 mean = {k: sum(v) / len(v) for k, v in agg.items()}
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
-from bench import lib_sha16  # noqa: E402  (the library these passes profiled: bench.py uses the
-#                                          traffic only while the loaded library has this hash)
+from bench import code_sha16, lib_sha16  # noqa: E402  (the library these passes profiled: bench.py uses
+#                                   the traffic only while the loaded library's device code has this hash)
 
-res = {"config": cfg, "source": note, "lib_sha16": lib_sha16(), "dispatches": {k: len(v) for k, v in agg.items()},
+res = {"config": cfg, "source": note, "lib_sha16": lib_sha16(), "code_sha16": code_sha16(), "dispatches": {k: len(v) for k, v in agg.items()},
        "counters_mean_per_dispatch": mean}
 if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
     fetch = mean["FETCH_SIZE"] * 1024 * 2

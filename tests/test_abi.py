@@ -84,7 +84,7 @@ def check(lib, p, dtype=0, causal=0):
 
 def test_abi_version(lib):
     lib.fa_abi_version.restype = ctypes.c_int
-    assert lib.fa_abi_version() == 7
+    assert lib.fa_abi_version() == 8
 
 
 def test_check_accepts_valid(lib):

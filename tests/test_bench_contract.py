@@ -2,8 +2,13 @@
 ran ("roofline.traffic is a stored constant"), and the roofline arithmetic uses the
 algorithmic FLOPs / bytes of DESIGN.md section 5. No GPU needed."""
 import json
+import os
+import shutil
+import subprocess
 import sys
 from pathlib import Path
+
+import pytest
 
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
@@ -11,40 +16,78 @@ sys.path.insert(0, str(ROOT))
 import bench  # noqa: E402
 
 
-def _fake_tree(tmp_path, lib_bytes: bytes, pmc: dict | None):
-    (tmp_path / "flash_attention_cute_amd" / "lib").mkdir(parents=True)
-    (tmp_path / "flash_attention_cute_amd" / "lib" / "libfa_gfx950.so").write_bytes(lib_bytes)
-    (tmp_path / "profiles").mkdir()
+_KERNEL = """#include <hip/hip_runtime.h>
+__global__ void k(float *x) { x[threadIdx.x] *= %s; }
+extern "C" int run(float *x, hipStream_t s) { hipLaunchKernelGGL(k, dim3(1), dim3(64), 0, s, x); return 0; }
+"""
+
+
+@pytest.fixture(scope="module")
+def tiny_libs(tmp_path_factory):
+    """Three gfx950 libraries built here by hipcc: a and b from the SAME source (two compiles), c from a
+    kernel with another constant."""
+    hipcc = Path(os.environ.get("ROCM_PATH", "/opt/rocm")) / "bin" / "hipcc"
+    if not hipcc.exists():
+        pytest.skip("hipcc not available")
+    d = tmp_path_factory.mktemp("tiny")
+    out = {}
+    for name, const in (("a", "2.f"), ("b", "2.f"), ("c", "3.f")):
+        src = d / f"{name}.hip"
+        src.write_text(_KERNEL % const)
+        subprocess.run([str(hipcc), "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", str(src), "-o",
+                        str(d / f"{name}.so")], check=True, capture_output=True)
+        out[name] = d / f"{name}.so"
+    return out
+
+
+def _fake_tree(tmp_path, lib: Path, pmc: dict | None):
+    (tmp_path / "flash_attention_cute_amd" / "lib").mkdir(parents=True, exist_ok=True)
+    shutil.copyfile(lib, tmp_path / "flash_attention_cute_amd" / "lib" / "libfa_gfx950.so")
+    (tmp_path / "profiles").mkdir(exist_ok=True)
     if pmc is not None:
         (tmp_path / "profiles" / "pmc_c2.json").write_text(json.dumps(pmc))
 
 
-def test_traffic_is_used_only_for_the_profiled_library(tmp_path, monkeypatch):
+def test_device_code_hash_survives_a_rebuild(tiny_libs):
+    """Two compiles of one source differ as files (hipcc's per-compile ids) but not in device code;
+    another kernel differs in both ("traffic provenance breaks on any rebuild")."""
+    a, b, c = (tiny_libs[n] for n in "abc")
+    assert bench.lib_sha16(a) != bench.lib_sha16(b)
+    assert bench.code_sha16(a) == bench.code_sha16(b)
+    assert bench.code_sha16(a) != bench.code_sha16(c)
+    assert all(len(bench.code_sha16(x)) == 16 for x in (a, b, c))
+
+
+def test_traffic_is_used_only_for_the_profiled_device_code(tmp_path, monkeypatch, tiny_libs):
     monkeypatch.setattr(bench, "ROOT", tmp_path)
-    _fake_tree(tmp_path, b"library A", None)
-    sha = bench.lib_sha16()
-    assert len(sha) == 16
-    (tmp_path / "profiles" / "pmc_c2.json").write_text(json.dumps({"lib_sha16": sha, "hbm_bytes_per_launch": 123.0}))
+    _fake_tree(tmp_path, tiny_libs["a"], None)
+    code = bench.code_sha16()
+    (tmp_path / "profiles" / "pmc_c2.json").write_text(
+        json.dumps({"lib_sha16": bench.lib_sha16(), "code_sha16": code, "hbm_bytes_per_launch": 123.0}))
     traffic, why = bench.load_traffic("c2")
     assert traffic == 123.0 and why["traffic_stale"] is False
-    # the library changes, the committed PMC file does not: no stale number, and the reason says why
-    (tmp_path / "flash_attention_cute_amd" / "lib" / "libfa_gfx950.so").write_bytes(b"library B")
+    # a rebuild of the same source: another file, the same device code -> still this traffic
+    _fake_tree(tmp_path, tiny_libs["b"], None)
+    traffic, why = bench.load_traffic("c2")
+    assert traffic == 123.0 and why["traffic_stale"] is False
+    # other device code, the committed PMC file unchanged: no stale number, and the reason says why
+    _fake_tree(tmp_path, tiny_libs["c"], None)
     traffic, why = bench.load_traffic("c2")
     assert traffic is None and why["traffic_stale"] is True
-    assert why["traffic_profiled_lib"] == sha and why["traffic_this_lib"] != sha
+    assert why["traffic_profiled_lib"] == code and why["traffic_this_lib"] != code
     assert why["traffic_of_profiled_lib"] == 123.0
 
 
-def test_traffic_absent_without_a_pmc_file(tmp_path, monkeypatch):
+def test_traffic_absent_without_a_pmc_file(tmp_path, monkeypatch, tiny_libs):
     monkeypatch.setattr(bench, "ROOT", tmp_path)
-    _fake_tree(tmp_path, b"library", None)
+    _fake_tree(tmp_path, tiny_libs["a"], None)
     assert bench.load_traffic("c2") == (None, {"traffic_source": None})
 
 
 def test_committed_pmc_files_carry_a_library_hash():
     for p in sorted((ROOT / "profiles").glob("pmc_*.json")):
         d = json.loads(p.read_text())
-        assert len(d.get("lib_sha16", "")) == 16, p.name
+        assert len(d.get("lib_sha16", "")) == 16 and len(d.get("code_sha16", "0" * 16)) == 16, p.name
         assert d["hbm_bytes_per_launch"] > 0, p.name
 
 

@@ -551,3 +551,143 @@ def test_key_split_under_graph_capture(device):
         _debug.set_split()
     assert all(torch.equal(o, eager) for o in outs)
     assert m.split_errors() == 0
+
+
+@pytest.mark.parametrize("layout", ["halves", "pairs"])
+def test_key_split_timeout_leaves_the_next_launch_correct(device, layout):
+    """A hand-off that times out (debug library: wave 0 of the last q-tile of (batch 0, q-head 0) holds
+    its ready mark until its partner has abandoned the pair) is counted exactly once, and the NEXT
+    launches on the same stream are correct against the oracle with no further error: the abandoned
+    pair's arrivals word was left 0, so no launch inherits a stale ready mark (fa_fwd_w4 key-split
+    hand-off). Reference behaviour kept by the good launches: plain blocks, template.cuh:516-563."""
+    from flash_attention_cute_amd import _debug
+
+    shape = (1, 4, 2, 1024, 1024, 128) if layout == "halves" else (1, 16, 4, 4096, 4096, 128)
+    b, hq, hkv, sq, sk, d = shape
+    dtype = torch.float16
+    q, k, v = make(b, hq, hkv, sq, sk, d, dtype, zlib.crc32(repr((shape, "fault")).encode()))
+    qd, kd, vd = q.to(device), k.to(device), v.to(device)
+    dl = _debug.lib(debug=True)
+    _debug.set_split(2, debug=True)
+    _debug.set_split_pairs(1 if layout == "pairs" else 0, debug=True)
+    dl.fa_split_errors(1)
+    try:
+        _debug.set_split_fault(True)
+        bad = _debug.forward(qd, kd, vd, causal=True, variant="w4", workspace=True)
+        assert _debug.last_path(debug=True) == "w4" and _debug.last_layout(debug=True) == "split"
+        assert (dl.fa_debug_last_zigzag() == 3) == (layout == "pairs")
+        torch.cuda.synchronize()
+        assert dl.fa_split_errors(0) == 1
+        _debug.set_split_fault(False)
+        good = _debug.forward(qd, kd, vd, causal=True, variant="w4", workspace=True)
+        again = _debug.forward(qd, kd, vd, causal=True, variant="w4", workspace=True)
+        torch.cuda.synchronize()
+        assert dl.fa_split_errors(1) == 1  # (nothing new: the faulted pair left its word zeroed)
+    finally:
+        _debug.set_split_fault(False)
+        _debug.set_split(debug=True)
+        _debug.set_split_pairs(debug=True)
+        _debug.set_knobs(debug=True)
+    assert torch.equal(good, again)
+    check(good, q, k, v, d ** -0.5, True, dtype)
+    # the faulted launch can differ from the good one only in the abandoned block's rows (wave 0 of
+    # q-tile nq - 1 of (batch 0, q-head 0): rows 0-31 and 128-159 of that 256-row block; the partner's
+    # records are usually written by the time it gives up, so they may well be right)
+    nq = (sq + 255) // 256
+    for bb, hh, m in (bad.float() != good.float()).any(dim=-1).nonzero().tolist():
+        assert (bb, hh) == (0, 0) and m // 256 == nq - 1 and (m % 256) % 128 < 32, (bb, hh, m)
+
+
+def test_split_layouts_need_same_xcd_placement(device):
+    """With an XCD count that does not divide 8 (knob), the dispatcher takes the layouts without a
+    hand-off: causal prefill runs zigzag and asks for no workspace, split-KV decode merges in the
+    separate combine launch; both equal their placement-checked counterparts within the bar."""
+    import flash_attention_cute_amd as m
+    from flash_attention_cute_amd import _debug
+
+    q, k, v = (t.to(device) for t in make(1, 4, 2, 1024, 1024, 128, torch.float16, 31))
+    qd, kd, vd = (t.to(device) for t in make(1, 8, 1, 1, 65536, 128, torch.bfloat16, 32))
+    _debug.set_knobs()
+    _debug.set_split(2)
+    try:
+        split = m.flash_attn_func(q, k, v, causal=True)
+        assert _debug.last_layout() == "split"
+        dec = m.flash_attn_func(qd, kd, vd)
+        assert _debug.last_path() == "decode_split" and _debug.last_dec_fused()
+        _debug.set_xccs(3)
+        fallback = m.flash_attn_func(q, k, v, causal=True)
+        assert _debug.last_layout() == "zigzag"
+        dec_fb = m.flash_attn_func(qd, kd, vd)
+        assert _debug.last_path() == "decode_split" and not _debug.last_dec_fused()
+        _debug.set_xccs(4)  # (DPX-like: 4 XCDs, b and b + 8 still share one)
+        m.flash_attn_func(q, k, v, causal=True)
+        assert _debug.last_layout() == "split"
+        torch.cuda.synchronize()
+    finally:
+        _debug.set_xccs()
+        _debug.set_split()
+    assert (split.float() - fallback.float()).abs().max().item() < 4e-3
+    assert (dec.float() - dec_fb.float()).abs().max().item() < 3e-2
+
+
+def test_first_key_split_call_beside_a_graph_capture(device):
+    """A stream's first key-split / fused-decode call allocates its counter area (hipMalloc with the
+    thread in relaxed capture mode) and zeroes it with a memset on that stream -- no device-wide
+    synchronisation -- so it may run while another stream is capturing a graph in global mode (torch's
+    default); the captured graph, which never holds a shared area, replays bit-identical to its eager
+    launch. The side-stream calls go through the C-ABI with buffers allocated beforehand (torch's own
+    caching allocator is not what is tested here)."""
+    import ctypes
+
+    import flash_attention_cute_amd as m
+    from flash_attention_cute_amd import _debug
+
+    lib = _debug.lib()
+    q, k, v = (t.to(device) for t in make(1, 4, 2, 1024, 1024, 128, torch.float16, 41))
+    qd, kd, vd = (t.to(device) for t in make(1, 8, 1, 1, 65536, 128, torch.float16, 42))
+    _debug.set_split(2)
+    m.split_errors(reset=True)
+
+    def abi_call(qx, kx, vx, causal, stream):
+        """fa_fwd_gfx950_ws on `stream` with preallocated output and workspace (the op's host steps:
+        Sq == 1 q-head pack for decode)."""
+        b, hq, sq, d = qx.shape
+        hkv = kx.size(1)
+        pack = sq == 1
+        qp = qx.reshape(b, hkv, hq // hkv, d) if pack else qx
+        o = torch.empty_like(qp)
+        p = _debug.FaFwdParams(qp.data_ptr(), kx.data_ptr(), vx.data_ptr(), o.data_ptr(), b, qp.size(1), hkv,
+                               qp.size(2), kx.size(2), d, 1 if pack else hq // hkv,
+                               *(t.stride(i) for i in range(3) for t in (qp, kx, vx, o)), d ** -0.5 * _debug.LOG2E)
+        need = lib.fa_fwd_gfx950_workspace_size(ctypes.byref(p), 0, int(causal))
+        ws = torch.empty(max(need, 16), dtype=torch.uint8, device=device)
+        run = lambda: lib.fa_fwd_gfx950_ws(ctypes.byref(p), 0, int(causal), ws.data_ptr(), need,  # noqa: E731
+                                           ctypes.c_void_p(stream.cuda_stream))
+        return run, o.reshape(qx.shape)
+
+    try:
+        eager = m.flash_attn_func(q, k, v, causal=True)
+        eager_dec = m.flash_attn_func(qd, kd, vd)
+        side = torch.cuda.Stream()  # (new: no counter area yet)
+        run_pf, side_out = abi_call(q, k, v, True, side)
+        run_dec, side_dec = abi_call(qd, kd, vd, False, side)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = m.flash_attn_func(q, k, v, causal=True)
+            out_dec = m.flash_attn_func(qd, kd, vd)
+            assert not _debug.last_dec_fused()  # (under capture: the combine launch)
+            # an eager first call on another stream mid-capture: allocates that stream's area
+            assert run_pf() == 0 and _debug.last_layout() == "split"
+            assert run_dec() == 0 and _debug.last_dec_fused()
+        side.synchronize()
+        outs = []
+        for _ in range(3):
+            g.replay()
+            outs.append((out.clone(), out_dec.clone()))
+        torch.cuda.synchronize()
+    finally:
+        _debug.set_split()
+    assert torch.equal(side_out, eager) and torch.equal(side_dec, eager_dec)
+    assert all(torch.equal(o, eager) and torch.equal(od, eager_dec) for o, od in outs)
+    assert m.split_errors() == 0

@@ -211,23 +211,30 @@ def pairs_codes(*args):
     return gen(*args)
 
 
-def test_golden_pairs_case():
-    """The key-split pairs fixture (golden_pairs.npz: the reference op on a causal GQA launch that the
-    default rule runs as pairs; inputs regenerated from the stored seed): the restatement on the three
-    sampled q-heads reproduces the reference's sampled rows."""
-    g = np.load(GOLD / "golden_pairs.npz")
-    assert json.loads((GOLD / "golden_meta.json").read_text())["n_pairs_cases"] == 1
+PAIRS_FILES = json.loads((GOLD / "golden_meta.json").read_text())["pairs_files"]
+
+
+@pytest.mark.parametrize("fname", PAIRS_FILES)
+def test_golden_pairs_case(fname):
+    """The key-split pairs fixtures (golden_pairs.npz fp16, golden_pairs_bf16.npz bf16: the reference op
+    on a causal GQA launch that the default rule runs as pairs; inputs regenerated from the stored seed):
+    the restatement on the three sampled q-heads reproduces the reference's sampled rows."""
+    g = np.load(GOLD / fname)
+    meta = json.loads((GOLD / "golden_meta.json").read_text())
+    assert meta["n_pairs_cases"] == 2 and set(PAIRS_FILES) == {"golden_pairs.npz", "golden_pairs_bf16.npz"}
+    dtype = str(g["dtype"])
     b, hq, hkv, sq, sk, d, causal = (int(x) for x in g["meta"])
     qc, kc, vc = pairs_codes(int(g["seed"]), b, hq, hkv, sq, sk, d)
     cs, heads, rows = float(g["code_scale"]), g["heads"], g["rows"]
     grp = hq // hkv
     q = qc[:, heads].astype(np.float64) / cs
     k, v = (c[:, heads // grp].astype(np.float64) / cs for c in (kc, vc))
-    out = O.flash_attention_fwd(q, k, v, float(g["scale"]), bool(causal), "f16")[:, :, rows]
-    o = as_f64(g["o"], "f16")
+    out = O.flash_attention_fwd(q, k, v, float(g["scale"]), bool(causal), dtype)[:, :, rows]
+    o = as_f64(g["o"], dtype)
     assert out.shape == o.shape
-    np.testing.assert_allclose(out, o, atol=2e-3, rtol=2e-3)
-    assert np.abs(out - o).mean() < 2e-3 / 8
+    atol = {"f16": 2e-3, "bf16": 1.6e-2}[dtype]
+    np.testing.assert_allclose(out, o, atol=atol, rtol=atol)
+    assert np.abs(out - o).mean() < atol / 8
 
 
 def test_golden_gqa_covers_the_pack_and_the_mapping():
