@@ -19,8 +19,8 @@ import ctypes
 
 from . import _build
 
-PATHS = {0: "none", 1: "w4", 2: "w8", 3: "w4slow", 4: "decode", 5: "decode_split", 6: "p8"}
-VARIANTS = {"w4": 0, "w8": 1, "w4slow": 2, "p8": 3}
+PATHS = {0: "none", 1: "w4", 2: "w8", 3: "w4slow", 4: "decode", 5: "decode_split", 6: "p8", 7: "m32", 8: "m16"}
+VARIANTS = {"w4": 0, "w8": 1, "w4slow": 2, "p8": 3, "m32": 4, "m16": 5}
 LOG2E = 1.4426950408889634
 
 _libs = {}

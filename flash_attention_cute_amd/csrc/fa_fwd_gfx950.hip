@@ -39,7 +39,8 @@ thread_local int g_last_path = fa::kPathNone;
 fa::Knobs knobs_from_env() {
     fa::Knobs k{0, 0, 1, fa::kDecTargetWgs, fa::kDecNt, 1, 1, FA_SPLIT_PAIRS, FA_DEC_FUSE, 0, 0};
     if (const char *v = getenv("FA_GFX950_VARIANT"))
-        k.variant = !strcmp(v, "w8") ? 1 : !strcmp(v, "w4slow") ? 2 : !strcmp(v, "p8") ? 3 : 0;
+        k.variant = !strcmp(v, "w8") ? 1 : !strcmp(v, "w4slow") ? 2 : !strcmp(v, "p8") ? 3 : !strcmp(v, "m32") ? 4
+                  : !strcmp(v, "m16") ? 5 : 0;
     if (const char *e = getenv("FA_W4_GRID")) k.w4_grid = atoll(e) > 0 ? atoll(e) : 0;
     if (const char *e = getenv("FA_GFX950_DECODE")) k.decode = strcmp(e, "0") != 0;
     if (const char *e = getenv("FA_DEC_TARGET_WGS")) k.dec_target = atoll(e) > 0 ? atoll(e) : fa::kDecTargetWgs;
@@ -54,7 +55,9 @@ fa::Knobs knobs_from_env() {
         fprintf(stderr,
                 "[fa_gfx950] FA_GFX950_VARIANT=%s: prefill launches run the %s kernel instead of fa_fwd_w4 "
                 "(debug / A-B variant, not the product path)\n",
-                getenv("FA_GFX950_VARIANT"), k.variant == 1 ? "fa_fwd_w8" : k.variant == 2 ? "w4slow" : "fa_fwd_p8");
+                getenv("FA_GFX950_VARIANT"),
+                k.variant == 1 ? "fa_fwd_w8" : k.variant == 2 ? "w4slow" : k.variant == 3 ? "fa_fwd_p8"
+                : k.variant == 4 ? "fa_fwd_mb (32x32x16)" : "fa_fwd_mb (16x16x32)");
 #else
     if (k.variant != 0) {  // the product library compiles fa_fwd_w4 only
         fprintf(stderr,

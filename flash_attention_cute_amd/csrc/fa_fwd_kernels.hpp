@@ -2441,6 +2441,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
 // the paired 8-wave kernel (fa_fwd_p8.hpp)
 template <class DT, bool C, int kD, bool kExact>
 int launch_p8(const fa_fwd_params &p, hipStream_t stream);
+// the MFMA-shape A/B body (fa_fwd_mb.hpp): m16 = 16x16x32, else 32x32x16
+template <class DT, bool C, int kD, bool kExact>
+int launch_mb(const fa_fwd_params &p, hipStream_t stream, bool m16);
 #endif
 
 // ---- host launch of one instantiation -------------------------------------------------
@@ -2451,8 +2454,9 @@ int launch_one(const fa_fwd_params &p, const PathArgs &xa, hipStream_t stream) {
     // have none of them
 #ifdef FA_DEBUG_VARIANTS
     const bool w4_only = xa.k_rng || xa.cos || xa.window_left >= 0;
-    const int variant = w4_only && (variant_from_env() == 1 || variant_from_env() == 3) ? 0 : variant_from_env();
+    const int variant = w4_only && variant_from_env() != 2 ? 0 : variant_from_env();
     if (variant == 3) return launch_p8<DT, C, kD, kExact>(p, stream);
+    if (variant == 4 || variant == 5) return launch_mb<DT, C, kD, kExact>(p, stream, variant == 5);  // (unsplit)
 #else
     constexpr int variant = 0;  // the product library: fa_fwd_w4 only
 #endif

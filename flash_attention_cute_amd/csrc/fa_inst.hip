@@ -3,8 +3,9 @@
 // FA_INST_EXACT (0 | 1), in parallel, and links the objects with fa_fwd_gfx950.hip.
 #ifndef FA_INST_STUB
 #include "fa_fwd_kernels.hpp"
-#ifdef FA_DEBUG_VARIANTS  // (the debug / A-B library: the paired 8-wave body)
+#ifdef FA_DEBUG_VARIANTS  // (the debug / A-B library: the paired 8-wave body, the MFMA-shape A/B body)
 #include "fa_fwd_p8.hpp"
+#include "fa_fwd_mb.hpp"
 #endif
 #include "fa_decode.hpp"
 #else

@@ -33,7 +33,9 @@ int set_err(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3))
 //   variant    0 = fa_fwd_w4 (default); 1 = fa_fwd_w8 (FA_GFX950_VARIANT=w8: the 8-wave
 //              register-staged kernel, A/B and cross-check); 2 = w4 without its pipelined body
 //              (FA_GFX950_VARIANT=w4slow, debug); 3 = fa_fwd_p8 (FA_GFX950_VARIANT=p8: two waves per
-//              SIMD, dense prefill; varlen / RoPE stay on fa_fwd_w4)
+//              SIMD, dense prefill; varlen / RoPE stay on fa_fwd_w4); 4 / 5 = fa_fwd_mb with the
+//              32x32x16 / 16x16x32 MFMA (FA_GFX950_VARIANT=m32 / m16: the shape A/B body, dense
+//              prefill only, fa_fwd_mb.hpp)
 //   w4_grid    cap of the persistent fa_fwd_w4 grid (FA_W4_GRID; 0 = the CU count)
 //   decode     split-KV decode kernel for few rows per kv-head (FA_GFX950_DECODE=0 turns it off)
 //   dec_target workgroups the decode split plan aims at (FA_DEC_TARGET_WGS)
@@ -58,7 +60,8 @@ const Knobs &knobs();
 inline int variant_from_env() { return knobs().variant; }
 
 // Which kernel the last fa_fwd_gfx950* call on this thread launched (fa_debug_last_path)
-enum Path { kPathNone = 0, kPathW4 = 1, kPathW8 = 2, kPathW4Slow = 3, kPathDecode = 4, kPathDecodeSplit = 5, kPathP8 = 6 };
+enum Path { kPathNone = 0, kPathW4 = 1, kPathW8 = 2, kPathW4Slow = 3, kPathDecode = 4, kPathDecodeSplit = 5, kPathP8 = 6,
+            kPathM32 = 7, kPathM16 = 8 };
 void set_last_path(int path);
 void set_last_zigzag(int z);
 void set_last_dec_fused(bool fused);  // (fa_debug_last_dec_fused: the last decode launch merged in-kernel)

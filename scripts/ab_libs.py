@@ -2,7 +2,7 @@
 """Interleaved A/B timing of several builds of the C-ABI library on one bench config (same process,
 same device, same inputs), so device-to-device clock differences cancel out.
 usage: python scripts/ab_libs.py <cfg> <lib.so>[@variant] [...]   (env AB_REPS, AB_ITERS)
-       variant: w4 | w8 | w4slow | p8, set through the library's fa_debug_set_knobs before its runs
+       variant: w4 | w8 | w4slow | p8 | m32 | m16, set through the library's fa_debug_set_knobs before its runs
 """
 import ctypes
 import os
@@ -20,7 +20,7 @@ if os.environ.get("AB_SHAPE"):  # B,Hq,Hkv,S,D,dtype,causal: a shape of its own 
     b_, hq_, hkv_, s_, d_, dt_, c_ = os.environ["AB_SHAPE"].split(",")
     cfg.update(B=int(b_), Hq=int(hq_), Hkv=int(hkv_), Sq=int(s_), Sk=int(s_), D=int(d_), dtype=dt_, causal=c_ == "1")
     cfg.pop("W", None)
-VARIANTS = {"w4": 0, "w8": 1, "w4slow": 2, "p8": 3}
+VARIANTS = {"w4": 0, "w8": 1, "w4slow": 2, "p8": 3, "m32": 4, "m16": 5}
 specs = [a.split("@") for a in sys.argv[2:]]
 libs = [ctypes.CDLL(os.path.abspath(sp[0])) for sp in specs]
 variants = [VARIANTS[sp[1]] if len(sp) > 1 else -1 for sp in specs]

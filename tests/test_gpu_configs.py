@@ -220,6 +220,70 @@ def test_reference_module_path_pybind_call_matches_flash_attn_func(op, device, c
     assert torch.equal(a, d)
 
 
+
+@pytest.mark.parametrize("variant", ["m16", "m32"])
+def test_reference_golden_vectors_on_the_shape_bodies(device, variant):
+    """Every reference-produced fixture (golden_small / _multi / _gqa / _gqa128 / _pairs*) through the
+    MFMA-shape A/B body of the debug library (csrc/fa_fwd_mb.hpp): v_mfma_f32_16x16x32 ("m16") and its
+    32x32x16 twin ("m32") -- dense prefill for every case (the Sq == 1 pack included: the shape bodies
+    take no decode path), the fixtures' own tolerances."""
+    import sys
+
+    from flash_attention_cute_amd import _debug
+
+    sys.path.insert(0, str(GOLD))
+    from make_golden import pairs_codes
+
+    meta = json.loads((GOLD / "golden_meta.json").read_text())
+    tols = {"f16": 2e-3, "bf16": 1.6e-2}
+    cases = []  # (q, k, v, scale, causal, ref, dtype, pick)
+    g = np.load(GOLD / "golden_small.npz")
+    for i in range(meta["n_small_cases"]):
+        dtype = str(g[f"case{i}_dtype"])
+        if dtype != "f32":
+            q, k, v, ref = (_gold_tensor(g[f"case{i}_{n_}"], dtype) for n_ in "qkvo")
+            cases.append((q, k, v, float(g[f"case{i}_scale"]), bool(g[f"case{i}_meta"][4]), ref, dtype, None))
+    g = np.load(GOLD / "golden_multi.npz")
+    for i in range(meta["n_multi_cases"]):
+        dtype = str(g[f"case{i}_dtype"])
+        q, k, v, ref = (_gold_tensor(g[f"case{i}_{n_}"], dtype) for n_ in "qkvo")
+        if str(g[f"case{i}_layout"]) == "bshd":
+            q, k, v = (t.transpose(1, 2).contiguous().transpose(1, 2) for t in (q, k, v))
+        cases.append((q, k, v, None, bool(g[f"case{i}_meta"][5]), ref, dtype, None))
+    for fname, key in (("golden_gqa.npz", "n_gqa_cases"), ("golden_gqa128.npz", "n_gqa128_cases")):
+        g = np.load(GOLD / fname)
+        cs = float(g["code_scale"])
+        for i in range(meta[key]):
+            dtype = str(g[f"case{i}_dtype"])
+            tdt = torch.float16 if dtype == "f16" else torch.bfloat16
+            q, k, v = (torch.from_numpy(g[f"case{i}_{n_}c"]).to(tdt).div_(cs) for n_ in "qkv")
+            cases.append((q, k, v, None, bool(g[f"case{i}_meta"][6]), _gold_tensor(g[f"case{i}_o"], dtype), dtype, None))
+    for fname in meta["pairs_files"]:
+        g = np.load(GOLD / fname)
+        b, hq, hkv, sq, sk, d, causal = (int(x) for x in g["meta"])
+        dtype = str(g["dtype"])
+        tdt = torch.float16 if dtype == "f16" else torch.bfloat16
+        q, k, v = (torch.from_numpy(c).to(tdt).div_(float(g["code_scale"]))
+                   for c in pairs_codes(int(g["seed"]), b, hq, hkv, sq, sk, d))
+        pick = (torch.from_numpy(g["heads"]), torch.from_numpy(g["rows"]))
+        cases.append((q, k, v, None, bool(causal), _gold_tensor(g["o"], dtype), dtype, pick))
+    assert len(cases) == 5 + 11 + 5 + 5 + 2
+    try:
+        for i, (q, k, v, scale, causal, ref, dtype, pick) in enumerate(cases):
+            out = _debug.forward(q.to(device), k.to(device), v.to(device), scale, causal, variant=variant)
+            assert _debug.last_path(debug=True) == variant, (i, _debug.last_path(debug=True))
+            out = out.float().cpu()
+            if pick is not None:
+                out = out[:, pick[0]][:, :, pick[1]]
+            ref = ref.float()
+            tol = tols[dtype]
+            err = (out - ref).abs()
+            assert (err <= tol + tol * ref.abs()).all(), (i, err.max().item())
+            assert err.mean().item() < tol / 8, (i, err.mean().item())
+    finally:
+        _debug.set_knobs(debug=True)
+
+
 FULL = [  # (name, B, Hq, Hkv, S, dtype, causal)
     ("C2", 4, 32, 32, 4096, torch.float16, False),
     ("C3", 4, 32, 32, 8192, torch.bfloat16, True),

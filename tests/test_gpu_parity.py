@@ -43,7 +43,7 @@ class _Variant:
         return _debug.forward(q, k, v, softmax_scale, causal, variant=self.variant)
 
 
-@pytest.fixture(params=["w4", "w8", "w4slow", "p8"])
+@pytest.fixture(params=["w4", "w8", "w4slow", "p8", "m16", "m32"])
 def fa(device, request):
     """The public op (the product kernel w4), or one of the debug library's bodies (the 8-wave
     cross-check w8, the non-pipelined w4slow, the paired 8-wave p8). Function-scoped: the knobs are
