@@ -354,6 +354,10 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_mb(const fa_fwd_params p, const
                 const int t = kM16 ? (n >> 3) & 1 : 0;
                 mx[X][t] = (n == 0 || (kM16 && n == 8)) ? s[X][n] : fmaxf(mx[X][t], s[X][n]);
             }
+            // (pin: ties each unit's results to its place among the fenced MFMA steps -- without it, IR
+            // code sinking moves the softmax below phase 2's last MFMA, past the rescale branch)
+#pragma unroll
+            for (int t = 0; t < NQ; ++t) pin(mx[X][t]);
         };
         // the row max across the lanes that share a row, the deferred-rescale decision of the block
         // (branch-free: m moves for every row of the block when some row outgrew m + threshold), alpha
@@ -374,6 +378,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_mb(const fa_fwd_params p, const
                 m_[X][t] = m_new;
                 msc[X][t] = msc_new;
                 l_[X][t] *= alpha[X][t];
+                pin(msc[X][t]);
+                pin(alpha[X][t]);
+                pin(l_[X][t]);
             }
         };
         auto u_exp = [&](const int X, const int k) __attribute__((always_inline)) {
@@ -381,12 +388,18 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_mb(const fa_fwd_params p, const
             for (int n = 4 * k; n < 4 * k + 4; ++n) {
                 const int t = kM16 ? (n >> 3) & 1 : 0;
                 s[X][n] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[X][n], sc, -msc[X][t]));
+                pin(s[X][n]);
                 l_[X][t] += s[X][n];
+                pin(l_[X][t]);
             }
         };
         auto u_pack = [&](const int X, const int u) __attribute__((always_inline)) {
 #pragma unroll
-            for (int w = 0; w < 4; ++w) P[X][u][w] = DT::pack(s[X][8 * u + 2 * w], s[X][8 * u + 2 * w + 1]);
+            for (int w = 0; w < 4; ++w) {
+                uint32_t x = DT::pack(s[X][8 * u + 2 * w], s[X][8 * u + 2 * w + 1]);
+                pin(x);
+                P[X][u][w] = x;
+            }
         };
         // unit i: 0-3 A max, 4-7 B max, 8 A decision, 9-16 A exp, 17 B decision, 18-25 B exp, 26-29 A pack,
         // 30-33 B pack
