@@ -78,10 +78,13 @@ def _jobs() -> int:
 
 
 def _process_pool():
-    """Worker processes for the assembly gate (a pure-Python dataflow over each instantiation, seconds each)."""
+    """Worker processes for the assembly gate (a pure-Python dataflow over each instantiation, seconds each).
+    Spawned, not forked: a fork taken while the compile threads' pool still holds locks left the workers
+    hung (seen twice in round 6)."""
+    import multiprocessing
     from concurrent.futures import ProcessPoolExecutor
 
-    return ProcessPoolExecutor(max_workers=_jobs())
+    return ProcessPoolExecutor(max_workers=_jobs(), mp_context=multiprocessing.get_context("spawn"))
 
 
 def build_abi(force: bool = False, verbose: bool = False, stamps: bool = False, tag: str = "",
