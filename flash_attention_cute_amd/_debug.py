@@ -66,6 +66,8 @@ def lib(debug: bool = False) -> ctypes.CDLL:
         lib.fa_debug_set_split_fault.argtypes = [ctypes.c_int]
         lib.fa_debug_set_split_fault.restype = None
         lib.fa_debug_last_dec_fused.restype = ctypes.c_int
+        lib.fa_debug_set_head_pack.argtypes = [ctypes.c_int]
+        lib.fa_debug_set_head_pack.restype = None
         lib.fa_fwd_gfx950_workspace_size.restype = ctypes.c_int64
         lib.fa_fwd_gfx950_ws.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
                                          ctypes.c_void_p]
@@ -147,10 +149,16 @@ def last_dec_fused(debug: bool = False) -> bool:
     return lib(debug).fa_debug_last_dec_fused() == 1
 
 
+def set_head_pack(mode: int | None = None, debug: bool = False) -> None:
+    """Head-packed causal GQA blocks (4 q-heads per kv-head, one per wave, 64 rows; fa_launch.h
+    use_head_pack): 0 never, 1 on multi-round grids (the default), 2 wherever they apply; None restores it."""
+    lib(debug).fa_debug_set_head_pack(-1 if mode is None else int(mode))
+
+
 def last_layout(debug: bool = False) -> str:
-    """Causal block layout of the last prefill launch on this thread: "plain", "zigzag" or "split"
-    (key-split, as halves or as pairs: last_split_pairs)."""
-    return {0: "plain", 1: "zigzag", 2: "split", 3: "split"}[lib(debug).fa_debug_last_zigzag()]
+    """Causal block layout of the last prefill launch on this thread: "plain", "zigzag", "split"
+    (key-split, as halves or as pairs: last_split_pairs) or "headpack"."""
+    return {0: "plain", 1: "zigzag", 2: "split", 3: "split", 4: "headpack"}[lib(debug).fa_debug_last_zigzag()]
 
 
 def last_split_pairs(debug: bool = False) -> bool:

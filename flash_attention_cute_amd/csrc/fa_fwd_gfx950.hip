@@ -37,7 +37,7 @@ unsigned long long *g_stamps = nullptr;
 thread_local int g_last_path = fa::kPathNone;
 
 fa::Knobs knobs_from_env() {
-    fa::Knobs k{0, 0, 1, fa::kDecTargetWgs, fa::kDecNt, 1, 1, FA_SPLIT_PAIRS, FA_DEC_FUSE, 0, 0};
+    fa::Knobs k{0, 0, 1, fa::kDecTargetWgs, fa::kDecNt, 1, 1, FA_SPLIT_PAIRS, FA_DEC_FUSE, 0, FA_HEAD_PACK, 0};
     if (const char *v = getenv("FA_GFX950_VARIANT"))
         k.variant = !strcmp(v, "w8") ? 1 : !strcmp(v, "w4slow") ? 2 : !strcmp(v, "p8") ? 3 : !strcmp(v, "m32") ? 4
                   : !strcmp(v, "m16") ? 5 : 0;
@@ -50,6 +50,7 @@ fa::Knobs knobs_from_env() {
     if (const char *e = getenv("FA_SPLIT_PAIRS")) k.split_pairs = atoi(e);
     if (const char *e = getenv("FA_DEC_FUSE")) k.dec_fuse = atoi(e);
     if (const char *e = getenv("FA_XCCS")) k.xccs = atoi(e) > 0 ? atoi(e) : 0;
+    if (const char *e = getenv("FA_HEAD_PACK")) k.head_pack = atoi(e);
 #ifdef FA_DEBUG_VARIANTS
     if (k.variant != 0)  // a debug / A-B body replaces the product kernel for the whole process: say so
         fprintf(stderr,
@@ -129,9 +130,14 @@ extern "C" void fa_debug_set_split_fault(int on) {
     (void)on;
 #endif
 }
+// head-packed causal blocks knob (Knobs::head_pack, env FA_HEAD_PACK): 0 never, 1 (default) the rule of
+// use_head_pack, 2 wherever it applies; < 0 restores the environment / default value
+extern "C" void fa_debug_set_head_pack(int mode) {
+    knobs_mut().head_pack = mode < 0 ? env_defaults().head_pack : mode;
+}
 // zigzag knob (fa_launch.h Knobs::zigzag): 0 never, 1 when the blocks fit one round, 2 always; < 0
 // restores the environment / default value. fa_debug_last_zigzag: the causal block layout of the
-// last prefill launch on this thread: 0 plain, 1 zigzag, 2 key-split, 3 key-split pairs.
+// last prefill launch on this thread: 0 plain, 1 zigzag, 2 key-split, 3 key-split pairs, 4 head-packed.
 extern "C" void fa_debug_set_zigzag(int mode) {
     knobs_mut().zigzag = mode < 0 ? env_defaults().zigzag : mode;
 }
@@ -632,11 +638,14 @@ extern "C" int fa_fwd_gfx950_geometry(const fa_fwd_params *params, int causal, i
         if (workgroups) *workgroups = fa::decode_units(*params, a) * a.n_split;
         return FA_OK;
     }
-    const int64_t n_qtiles = fa::use_zigzag(*params, causal != 0, kNoPath) ? fa::zigzag_qtiles(params->seqlen_q)
-                                                                          : (params->seqlen_q + fa::kBlockM - 1) / fa::kBlockM;
+    // (head-packed blocks: (batch, kv-head, 64 rows) units of 4 q-heads x 64 rows)
+    const bool hpk = fa::use_head_pack(*params, causal != 0, kNoPath);
+    const bool zz = !hpk && fa::use_zigzag(*params, causal != 0, kNoPath);
+    const int64_t n_qtiles = zz ? fa::zigzag_qtiles(params->seqlen_q)
+                             : hpk ? (params->seqlen_q + 63) / 64 : (params->seqlen_q + fa::kBlockM - 1) / fa::kBlockM;
     if (block_m) *block_m = fa::kBlockM;
     if (block_n) *block_n = fa::kBlockN;
     if (threads) *threads = (fa::variant_from_env() == 1 || fa::variant_from_env() == 3 ? fa::kThreads : 256);
-    if (workgroups) *workgroups = n_qtiles * params->num_heads_q * params->batch_size;
+    if (workgroups) *workgroups = n_qtiles * (hpk ? params->num_heads_kv : params->num_heads_q) * params->batch_size;
     return FA_OK;
 }

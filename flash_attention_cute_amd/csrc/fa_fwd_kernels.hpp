@@ -1005,7 +1005,16 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // the XCD, snake-ordered (odd rounds reversed) so that a heavy-first causal order balances
     // without a work queue. The next block's Q fragments and first K tile are fetched while the
     // current block drains its pipeline and stores O.
-    const uint32_t nwg = (uint32_t)n_qtiles * (uint32_t)p.num_heads_q * (uint32_t)p.batch_size;
+    // Head-packed blocks (xa.head_pack, dense causal GQA with exactly 4 q-heads per kv-head, multi-round
+    // grids): a block is (batch, kv-head, 64-row q-tile), wave w runs q-head 4 kv-head + w on those
+    // 64 rows (block A the first 32, block B the next 32). Every row keeps its own 32-row group and
+    // tile order, so the output is the plain layout's bit for bit; but the causal diagonal of a block
+    // is ONE tile instead of four (plain 256-row blocks: 4 masked tiles, 2 of them A-dead), and no
+    // tile is A-dead. Units: (batch, kv-head) rows of n_qtiles (the host passes Sq / 64 q-tiles).
+    const bool hp = kCausal && xa.head_pack != 0;
+    const int heads_u = hp ? (int)p.num_heads_kv : (int)p.num_heads_q;  // head rows of the work order
+    const int grp_u = hp ? 1 : (int)p.head_q_per_group;                  // q-heads per K/V stream there
+    const uint32_t nwg = (uint32_t)n_qtiles * (uint32_t)heads_u * (uint32_t)p.batch_size;
     const uint32_t xcd = blockIdx.x & 7, cx = blockIdx.x >> 3;
     const uint32_t gx = (gridDim.x - xcd + 7) >> 3;  // workgroups of this XCD
     // key-split blocks (below): the XCD-aware order runs over units whose pieces meet in ONE XCD's
@@ -1052,7 +1061,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     };
     auto work_of = [&](const uint32_t k) __attribute__((always_inline)) {
         if (!spl)
-            return decode_work<kCausal>(nwg, xcd + 8 * k, n_qtiles, (int)p.num_heads_q, (int)p.head_q_per_group);
+            return decode_work<kCausal>(nwg, xcd + 8 * k, n_qtiles, heads_u, grp_u);
         Work w;
         if (pairs) {
             pair_item(k, w);
@@ -1095,6 +1104,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             const int nseg = (sq + 127) >> 7, sB = nseg - 1 - qtile;
             m0o = qtile << 7;
             rowbo = sB > qtile ? (sB - qtile) << 7 : (nseg - qtile) << 7;  // (no partner: rows past Sq)
+        } else if (hp) {
+            m0o = qtile * 64;
+            rowbo = 32;
         } else {
             m0o = qtile * kBlockM;
             rowbo = kRowB;
@@ -1112,8 +1124,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     const int wl = xa.window_left;
     int j_lo = 0, j_um = 0;
     auto set_block = [&](const Work wk) {
-        const int hq = wk.hq, b = wk.b;
-        const int hkv = hq / (int)p.head_q_per_group;
+        const int hq = hp ? wk.hq * (int)p.head_q_per_group + wave : wk.hq, b = wk.b;  // (hp: wk.hq is the kv-head)
+        const int hkv = hp ? wk.hq : hq / (int)p.head_q_per_group;
         int64_t qrow0 = (int64_t)b * p.q_batch_stride, krow0 = (int64_t)b * p.k_batch_stride;
         int64_t vrow0 = (int64_t)b * p.v_batch_stride, orow0 = (int64_t)b * p.o_batch_stride;
         if (xa.q_rng) {  // this batch row's query rows and keys: absolute rows (the host zeroes the
@@ -1141,12 +1153,12 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         // rows interleaved over the waves: block A = rows mw..mw+31 (the workgroup's first half),
         // block B = rows mw+rowB.. (its second half), so the last causal diagonal tiles hold no
         // score of any wave's block A (A-dead tiles, below)
-        mw = m0 + wave * 32;
+        mw = hp ? m0 : m0 + wave * 32;
         n_end = n_blocks;
         if (kCausal) {
             // the workgroup's last row: block B's (zigzag: block A's when B has no partner segment)
             const int last = min(m0 + rowB < Sq ? m0 + rowB + kRowB : m0 + kRowB, Sq);
-            const int x = diag + (zz ? last : min(m0 + kBlockM, Sq));
+            const int x = diag + (zz ? last : min(m0 + (hp ? 64 : kBlockM), Sq));
             const int nb = x <= 0 ? 0 : (x + kBlockN - 1) / kBlockN;
             n_end = min(nb, n_blocks);
         }
@@ -1251,8 +1263,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         }
         int m0n;
         geom_of(qtile_of(wk), sq, m0n, rb);
-        const int mwn = m0n + wave * 32;
-        const char *qbn = (const char *)p.q_ptr + 2 * (row0 + (int64_t)wk.hq * p.q_head_stride);
+        const int mwn = hp ? m0n : m0n + wave * 32;
+        const int hqn = hp ? wk.hq * (int)p.head_q_per_group + wave : wk.hq;
+        const char *qbn = (const char *)p.q_ptr + 2 * (row0 + (int64_t)hqn * p.q_head_stride);
         return make_rsrc_u(qbn + 2 * (int64_t)mwn * qs_, slab_bytes(min(sq - mwn, rb + 32), qs_, D));
     };
     // the next block (decoded once, in this block's prologue) and its Q pieces: qn of qnt issued
@@ -2011,8 +2024,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // workgroup's first half, m0 .. m0 + kRowB - 1): they run B only (MASKED 2, then 3)
     int jA = n_loop;
     if (kCausal) {
-        // the last visible key of block A (rows m0 .. m0 + 127 in both layouts)
-        const int x = min(Sk - 1, m0 + kRowB - 1 + diag);
+        // the last visible key of block A (rows m0 .. m0 + 127 in both layouts; head-packed m0 .. m0 + 31)
+        const int x = min(Sk - 1, m0 + (hp ? 31 : kRowB - 1) + diag);
         jA = x < 0 ? 0 : x / kBlockN + 1;
     }
     const int jb = j_lo + 1;
@@ -2464,12 +2477,16 @@ int launch_one(const fa_fwd_params &p, const PathArgs &xa, hipStream_t stream) {
     // (xa.split_ws), else zigzag Q blocks for a causal launch that fits one round
     PathArgs xz = xa;
     if (variant == 1) xz.split_ws = nullptr;
-    xz.zigzag = !xz.split_ws && variant != 1 && use_zigzag(p, C, xa) ? 1 : 0;
+    // (the default rules are disjoint: head-packed blocks on multi-round grids, zigzag on one-round ones;
+    // the head_pack knob 2 forces them over zigzag)
+    xz.head_pack = !xz.split_ws && variant != 1 && use_head_pack(p, C, xa) ? 1 : 0;
+    xz.zigzag = !xz.split_ws && !xz.head_pack && variant != 1 && use_zigzag(p, C, xa) ? 1 : 0;
     const int64_t n_plain = (p.seqlen_q + kBlockM - 1) / kBlockM;
     xz.split_pairs = xz.split_ws && use_split_pairs(p, device_cus()) ? 1 : 0;
     const int64_t n_pairs = (n_plain + 1) / 2 * p.num_heads_q * p.batch_size;
-    const int64_t n_qtiles = xz.split_ws ? 2 * n_plain : xz.zigzag ? zigzag_qtiles(p.seqlen_q) : n_plain;
-    const int64_t nwg = n_qtiles * p.num_heads_q * p.batch_size;
+    const int64_t n_qtiles = xz.split_ws ? 2 * n_plain : xz.zigzag ? zigzag_qtiles(p.seqlen_q)
+                           : xz.head_pack ? (p.seqlen_q + 63) / 64 : n_plain;
+    const int64_t nwg = n_qtiles * (xz.head_pack ? p.num_heads_kv : p.num_heads_q) * p.batch_size;
 #ifdef FA_DEBUG_VARIANTS
     if (variant == 1)
         hipLaunchKernelGGL((fa_fwd_w8<DT, C, kD, kExact>), dim3((uint32_t)nwg), dim3(kThreads), 0, stream, p,
@@ -2484,7 +2501,7 @@ int launch_one(const fa_fwd_params &p, const PathArgs &xa, hipStream_t stream) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "HIP launch failed: %s", hipGetErrorString(e));
     set_last_path(variant == 1 ? kPathW8 : variant == 2 ? kPathW4Slow : kPathW4);
-    set_last_zigzag(xz.split_ws ? 2 + xz.split_pairs : xz.zigzag);
+    set_last_zigzag(xz.split_ws ? 2 + xz.split_pairs : xz.head_pack ? 4 : xz.zigzag);
     return FA_OK;
 }
 

@@ -53,6 +53,7 @@ struct Knobs {
     int split_pairs;  // key-split pairs (use_split_pairs): 0 never, 1 where they fit one pass (default)
     int dec_fuse;     // split-KV decode: 1 the last split of a unit merges (default), 0 fa_decode_combine
     int xccs;         // XCDs per device for the placement check (0: the device's own count; tests)
+    int head_pack;    // head-packed causal GQA blocks (use_head_pack): 0 never, 1 the rule (default), 2 always
     int split_fault;  // (debug library only) force one key-split hand-off to time out (kernel dbg & 2)
 };
 
@@ -131,6 +132,7 @@ struct PathArgs {
     unsigned *split_sync;
     unsigned *split_err;
     int split_pairs;
+    int head_pack;  // (set by launch_one, use_head_pack) head-packed causal blocks (fa_fwd_w4)
 };
 
 // Whether a prefill launch runs zigzag Q blocks, and its logical q-tile count (blocks per (batch,
@@ -145,6 +147,21 @@ inline bool use_zigzag(const fa_fwd_params &p, bool causal, const PathArgs &xa) 
     return knobs().zigzag == 2 || nwg <= device_cus();
 }
 inline int64_t zigzag_qtiles(int64_t seqlen_q) { return ((seqlen_q + 127) / 128 + 1) / 2; }
+
+// Head-packed causal blocks (fa_fwd_w4 "Head-packed blocks"): dense causal GQA with exactly 4 q-heads
+// per kv-head (one per wave: Llama-3-8B, C4, C5), more than one 64-row q-tile, when neither zigzag nor
+// key-split takes the launch (multi-round grids). A block is (batch, kv-head, 64 rows): its causal
+// diagonal is one tile instead of the plain 256-row block's four, two of them A-dead; bit-identical
+// to the plain layout. Knob head_pack (env FA_HEAD_PACK): 0 never, 1 by this rule (default), 2 whenever
+// it applies (also one-round grids, tests).
+inline bool use_head_pack(const fa_fwd_params &p, bool causal, const PathArgs &xa) {
+    if (!causal || xa.k_rng || xa.cos || xa.window_left >= 0 || knobs().head_pack == 0) return false;
+    if (p.head_q_per_group != 4 || p.seqlen_q <= 64) return false;
+    if (knobs().head_pack == 2) return true;
+    if (knobs().zigzag == 2 && use_zigzag(p, causal, xa)) return false;  // (a forced zigzag wins over the rule)
+    const int64_t nwg = (p.seqlen_q + kBlockM - 1) / kBlockM * p.num_heads_q * p.batch_size;
+    return nwg > device_cus();
+}
 
 // Key-split causal blocks: dense causal launches (no varlen, window or RoPE) when the caller passes
 // the workspace. Knob 1 (default): where measured faster than zigzag (profiles/r4_split_sweep.log,
@@ -171,6 +188,9 @@ inline int64_t split_wave_floats(int64_t headdim) {
 // XCD. Knob split_pairs (env FA_SPLIT_PAIRS): 0 never, 1 where this holds (default).
 #ifndef FA_SPLIT_PAIRS
 #define FA_SPLIT_PAIRS 1
+#endif
+#ifndef FA_HEAD_PACK  // default of Knobs::head_pack
+#define FA_HEAD_PACK 1
 #endif
 #ifndef FA_DEC_FUSE  // default of Knobs::dec_fuse
 #define FA_DEC_FUSE 1

@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Interleaved A/B timing of several builds of the C-ABI library on one bench config (same process,
 same device, same inputs), so device-to-device clock differences cancel out.
-usage: python scripts/ab_libs.py <cfg> <lib.so>[@variant] [...]   (env AB_REPS, AB_ITERS)
-       variant: w4 | w8 | w4slow | p8 | m32 | m16, set through the library's fa_debug_set_knobs before its runs
+usage: python scripts/ab_libs.py <cfg> <lib.so>[@variant[:knob=value,...]] [...]   (env AB_REPS, AB_ITERS)
+       variant: w4 | w8 | w4slow | p8 | m32 | m16, set through the library's fa_debug_set_knobs before its runs;
+       knobs (debug setters of that library, applied before its runs): hp (head-packed blocks), zz (zigzag),
+       split, pairs. A library named twice is loaded from a copy, so each entry keeps its own knobs.
 """
 import ctypes
 import os
@@ -21,9 +23,26 @@ if os.environ.get("AB_SHAPE"):  # B,Hq,Hkv,S,D,dtype,causal: a shape of its own 
     cfg.update(B=int(b_), Hq=int(hq_), Hkv=int(hkv_), Sq=int(s_), Sk=int(s_), D=int(d_), dtype=dt_, causal=c_ == "1")
     cfg.pop("W", None)
 VARIANTS = {"w4": 0, "w8": 1, "w4slow": 2, "p8": 3, "m32": 4, "m16": 5}
+SETTERS = {"hp": "fa_debug_set_head_pack", "zz": "fa_debug_set_zigzag", "split": "fa_debug_set_split",
+           "pairs": "fa_debug_set_split_pairs"}
 specs = [a.split("@") for a in sys.argv[2:]]
-libs = [ctypes.CDLL(os.path.abspath(sp[0])) for sp in specs]
-variants = [VARIANTS[sp[1]] if len(sp) > 1 else -1 for sp in specs]
+libs, seen = [], set()
+for i, sp in enumerate(specs):
+    path = os.path.abspath(sp[0])
+    if path in seen:  # (dlopen of the same path returns the same handle and its knobs: load a copy)
+        import shutil
+        copy = f"/tmp/ab_libs_copy_{os.getpid()}_{i}.so"
+        shutil.copyfile(path, copy)
+        path = copy
+    seen.add(os.path.abspath(sp[0]))
+    libs.append(ctypes.CDLL(path))
+variants = [VARIANTS[sp[1].split(":")[0] or "w4"] if len(sp) > 1 else -1 for sp in specs]
+knob_sets = [[kv.split("=") for kv in sp[1].split(":")[1].split(",")] if len(sp) > 1 and ":" in sp[1] else []
+             for sp in specs]
+for lib, ks in zip(libs, knob_sets):
+    for k, v in ks:
+        getattr(lib, SETTERS[k]).argtypes = [ctypes.c_int]
+        getattr(lib, SETTERS[k])(int(v))
 
 
 class P(ctypes.Structure):

@@ -691,3 +691,66 @@ def test_first_key_split_call_beside_a_graph_capture(device):
     assert torch.equal(side_out, eager) and torch.equal(side_dec, eager_dec)
     assert all(torch.equal(o, eager) and torch.equal(od, eager_dec) for o, od in outs)
     assert m.split_errors() == 0
+
+
+HEADPACK = [  # (B, Hq, Hkv, Sq, Sk, D): causal GQA with 4 q-heads per kv-head
+    (1, 8, 2, 1024, 1024, 128),
+    (2, 4, 1, 300, 300, 128),     # ragged: a 44-row last q-tile
+    (1, 4, 1, 700, 1500, 128),    # Sq < Sk
+    (1, 8, 2, 1500, 700, 64),     # Sq > Sk: the first rows see no key (output 0)
+    (1, 4, 1, 130, 130, 64),      # three 64-row q-tiles, one key tile
+]
+
+
+@pytest.mark.parametrize("shape", HEADPACK, ids=[str(s) for s in HEADPACK])
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16], ids=["f16", "bf16"])
+def test_head_packed_blocks(device, shape, dtype):
+    """Head-packed causal blocks (fa_fwd_w4 "Head-packed blocks": a block is (batch, kv-head, 64 rows),
+    wave w on q-head 4 kv-head + w), forced with knob 2: against the oracle, and BIT-identical to the
+    plain 256-row layout -- every row keeps its 32-row group and its tile order."""
+    import flash_attention_cute_amd as m
+    from flash_attention_cute_amd import _debug
+
+    b, hq, hkv, sq, sk, d = shape
+    q, k, v = make(b, hq, hkv, sq, sk, d, dtype, zlib.crc32(repr((shape, str(dtype), "hp")).encode()))
+    qd, kd, vd = q.to(device), k.to(device), v.to(device)
+    _debug.set_knobs()
+    try:
+        _debug.set_head_pack(2)
+        out = m.flash_attn_func(qd, kd, vd, causal=True)
+        assert _debug.last_path() == "w4" and _debug.last_layout() == "headpack"
+        with _debug.knobs(w4_grid=8):  # many rounds per workgroup
+            small = m.flash_attn_func(qd, kd, vd, causal=True)
+        _debug.set_head_pack(0)
+        _debug.set_zigzag(0)
+        _debug.set_split(0)
+        plain = m.flash_attn_func(qd, kd, vd, causal=True)
+        assert _debug.last_layout() == "plain"
+        torch.cuda.synchronize()
+    finally:
+        _debug.set_head_pack()
+        _debug.set_zigzag()
+        _debug.set_split()
+    assert torch.equal(out, plain) and torch.equal(out, small)
+    check(out, q, k, v, d ** -0.5, True, dtype)
+
+
+def test_head_packed_blocks_by_default(device):
+    """The default rule: multi-round causal grids with g = 4 take head-packed blocks (C4 / C5's class);
+    g = 2, non-causal, and one-round grids (zigzag / key-split) do not."""
+    import flash_attention_cute_amd as m
+    from flash_attention_cute_amd import _debug
+
+    _debug.set_knobs()
+    _debug.set_head_pack()
+    big = [torch.randn(2, h, 2048, 128, device=device, dtype=torch.float16) for h in (32, 8, 8)]  # 512 blocks
+    m.flash_attn_func(*big, causal=True)
+    assert _debug.last_layout() == "headpack"
+    m.flash_attn_func(*big, causal=False)
+    assert _debug.last_layout() == "plain"
+    g2 = [torch.randn(2, h, 2048, 128, device=device, dtype=torch.float16) for h in (32, 16, 16)]
+    m.flash_attn_func(*g2, causal=True)
+    assert _debug.last_layout() != "headpack"
+    one = [torch.randn(1, h, 1024, 128, device=device, dtype=torch.float16) for h in (8, 2, 2)]  # 32 blocks
+    m.flash_attn_func(*one, causal=True)
+    assert _debug.last_layout() in ("zigzag", "split")
