@@ -638,7 +638,7 @@ extern "C" int fa_fwd_gfx950_geometry(const fa_fwd_params *params, int causal, i
         if (workgroups) *workgroups = fa::decode_units(*params, a) * a.n_split;
         return FA_OK;
     }
-    // (head-packed blocks: (batch, kv-head, 64 rows) units of 4 q-heads x 64 rows)
+    // (head-packed blocks: (batch, q-head quad, 64 rows) units of 4 q-heads x 64 rows)
     const bool hpk = fa::use_head_pack(*params, causal != 0, kNoPath);
     const bool zz = !hpk && fa::use_zigzag(*params, causal != 0, kNoPath);
     const int64_t n_qtiles = zz ? fa::zigzag_qtiles(params->seqlen_q)
@@ -646,6 +646,6 @@ extern "C" int fa_fwd_gfx950_geometry(const fa_fwd_params *params, int causal, i
     if (block_m) *block_m = fa::kBlockM;
     if (block_n) *block_n = fa::kBlockN;
     if (threads) *threads = (fa::variant_from_env() == 1 || fa::variant_from_env() == 3 ? fa::kThreads : 256);
-    if (workgroups) *workgroups = n_qtiles * (hpk ? params->num_heads_kv : params->num_heads_q) * params->batch_size;
+    if (workgroups) *workgroups = n_qtiles * (hpk ? params->num_heads_q / 4 : params->num_heads_q) * params->batch_size;
     return FA_OK;
 }

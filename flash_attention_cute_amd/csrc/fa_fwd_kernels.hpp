@@ -1005,15 +1005,16 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // the XCD, snake-ordered (odd rounds reversed) so that a heavy-first causal order balances
     // without a work queue. The next block's Q fragments and first K tile are fetched while the
     // current block drains its pipeline and stores O.
-    // Head-packed blocks (xa.head_pack, dense causal GQA with exactly 4 q-heads per kv-head, multi-round
-    // grids): a block is (batch, kv-head, 64-row q-tile), wave w runs q-head 4 kv-head + w on those
-    // 64 rows (block A the first 32, block B the next 32). Every row keeps its own 32-row group and
-    // tile order, so the output is the plain layout's bit for bit; but the causal diagonal of a block
-    // is ONE tile instead of four (plain 256-row blocks: 4 masked tiles, 2 of them A-dead), and no
-    // tile is A-dead. Units: (batch, kv-head) rows of n_qtiles (the host passes Sq / 64 q-tiles).
+    // Head-packed blocks (xa.head_pack, dense causal GQA with a multiple of 4 q-heads per kv-head,
+    // multi-round grids): a block is (batch, 4 consecutive q-heads of one kv group, 64-row q-tile),
+    // wave w runs q-head 4 u + w on those 64 rows (block A the first 32, block B the next 32). Every
+    // row keeps its own 32-row group and tile order, so the output is the plain layout's bit for bit;
+    // but the causal diagonal of a block is ONE tile instead of four (plain 256-row blocks: 4 masked
+    // tiles, 2 of them A-dead), and no tile is A-dead. Units: (batch, q-head quad u) rows of n_qtiles
+    // (the host passes Sq / 64 q-tiles); g / 4 quads share a K/V stream.
     const bool hp = kCausal && xa.head_pack != 0;
-    const int heads_u = hp ? (int)p.num_heads_kv : (int)p.num_heads_q;  // head rows of the work order
-    const int grp_u = hp ? 1 : (int)p.head_q_per_group;                  // q-heads per K/V stream there
+    const int heads_u = hp ? (int)p.num_heads_q / 4 : (int)p.num_heads_q;             // head rows of the work order
+    const int grp_u = hp ? (int)p.head_q_per_group / 4 : (int)p.head_q_per_group;  // of them per K/V stream
     const uint32_t nwg = (uint32_t)n_qtiles * (uint32_t)heads_u * (uint32_t)p.batch_size;
     const uint32_t xcd = blockIdx.x & 7, cx = blockIdx.x >> 3;
     const uint32_t gx = (gridDim.x - xcd + 7) >> 3;  // workgroups of this XCD
@@ -1124,8 +1125,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     const int wl = xa.window_left;
     int j_lo = 0, j_um = 0;
     auto set_block = [&](const Work wk) {
-        const int hq = hp ? wk.hq * (int)p.head_q_per_group + wave : wk.hq, b = wk.b;  // (hp: wk.hq is the kv-head)
-        const int hkv = hp ? wk.hq : hq / (int)p.head_q_per_group;
+        const int hq = hp ? 4 * wk.hq + wave : wk.hq, b = wk.b;  // (hp: wk.hq is the q-head quad)
+        const int hkv = hq / (int)p.head_q_per_group;
         int64_t qrow0 = (int64_t)b * p.q_batch_stride, krow0 = (int64_t)b * p.k_batch_stride;
         int64_t vrow0 = (int64_t)b * p.v_batch_stride, orow0 = (int64_t)b * p.o_batch_stride;
         if (xa.q_rng) {  // this batch row's query rows and keys: absolute rows (the host zeroes the
@@ -1264,7 +1265,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         int m0n;
         geom_of(qtile_of(wk), sq, m0n, rb);
         const int mwn = hp ? m0n : m0n + wave * 32;
-        const int hqn = hp ? wk.hq * (int)p.head_q_per_group + wave : wk.hq;
+        const int hqn = hp ? 4 * wk.hq + wave : wk.hq;
         const char *qbn = (const char *)p.q_ptr + 2 * (row0 + (int64_t)hqn * p.q_head_stride);
         return make_rsrc_u(qbn + 2 * (int64_t)mwn * qs_, slab_bytes(min(sq - mwn, rb + 32), qs_, D));
     };
@@ -2486,7 +2487,7 @@ int launch_one(const fa_fwd_params &p, const PathArgs &xa, hipStream_t stream) {
     const int64_t n_pairs = (n_plain + 1) / 2 * p.num_heads_q * p.batch_size;
     const int64_t n_qtiles = xz.split_ws ? 2 * n_plain : xz.zigzag ? zigzag_qtiles(p.seqlen_q)
                            : xz.head_pack ? (p.seqlen_q + 63) / 64 : n_plain;
-    const int64_t nwg = n_qtiles * (xz.head_pack ? p.num_heads_kv : p.num_heads_q) * p.batch_size;
+    const int64_t nwg = n_qtiles * (xz.head_pack ? p.num_heads_q / 4 : p.num_heads_q) * p.batch_size;
 #ifdef FA_DEBUG_VARIANTS
     if (variant == 1)
         hipLaunchKernelGGL((fa_fwd_w8<DT, C, kD, kExact>), dim3((uint32_t)nwg), dim3(kThreads), 0, stream, p,

@@ -693,12 +693,13 @@ def test_first_key_split_call_beside_a_graph_capture(device):
     assert m.split_errors() == 0
 
 
-HEADPACK = [  # (B, Hq, Hkv, Sq, Sk, D): causal GQA with 4 q-heads per kv-head
+HEADPACK = [  # (B, Hq, Hkv, Sq, Sk, D): causal GQA with a multiple of 4 q-heads per kv-head
     (1, 8, 2, 1024, 1024, 128),
     (2, 4, 1, 300, 300, 128),     # ragged: a 44-row last q-tile
     (1, 4, 1, 700, 1500, 128),    # Sq < Sk
     (1, 8, 2, 1500, 700, 64),     # Sq > Sk: the first rows see no key (output 0)
     (1, 4, 1, 130, 130, 64),      # three 64-row q-tiles, one key tile
+    (1, 16, 2, 600, 600, 128),    # g = 8: two q-head quads per kv group
 ]
 
 
@@ -737,7 +738,8 @@ def test_head_packed_blocks(device, shape, dtype):
 
 def test_head_packed_blocks_by_default(device):
     """The default rule: multi-round causal grids with g = 4 take head-packed blocks (C4 / C5's class);
-    g = 2, non-causal, and one-round grids (zigzag / key-split) do not."""
+    g = 8 too (two q-head quads per kv group); g = 2, non-causal, and one-round grids (zigzag /
+    key-split) do not."""
     import flash_attention_cute_amd as m
     from flash_attention_cute_amd import _debug
 
@@ -751,6 +753,9 @@ def test_head_packed_blocks_by_default(device):
     g2 = [torch.randn(2, h, 2048, 128, device=device, dtype=torch.float16) for h in (32, 16, 16)]
     m.flash_attn_func(*g2, causal=True)
     assert _debug.last_layout() != "headpack"
+    g8 = [torch.randn(2, h, 2048, 128, device=device, dtype=torch.float16) for h in (32, 4, 4)]
+    m.flash_attn_func(*g8, causal=True)
+    assert _debug.last_layout() == "headpack"
     one = [torch.randn(1, h, 1024, 128, device=device, dtype=torch.float16) for h in (8, 2, 2)]  # 32 blocks
     m.flash_attn_func(*one, causal=True)
     assert _debug.last_layout() in ("zigzag", "split")

@@ -6,7 +6,8 @@ launches of the same inputs. DESIGN.md section 5 records one discarded experimen
 524k differed; this sweep checks ~0.8M rows of the kept kernel (fa_fwd_w4, persistent, several Q
 blocks per workgroup through a capped grid so every block switch -- Q staged by LDS-DMA, the
 first-tile rescale -- runs many times) and requires every row within the parity tolerance and two
-launches bit-identical. The same sweep runs the paired 8-wave variant fa_fwd_p8.
+launches bit-identical. The same sweep runs the head-packed causal layout (forced) and the paired
+8-wave variant fa_fwd_p8.
 """
 from __future__ import annotations
 
@@ -28,17 +29,17 @@ class _Op:
         from flash_attention_cute_amd import _debug
         from flash_attention_cute_amd import flash_attn_func
 
-        if self.variant == "w4":  # the product op
+        if self.variant in ("w4", "w4hp"):  # the product op (w4hp: head-packed causal blocks forced)
             return flash_attn_func(q, k, v, causal=causal)
         return _debug.forward(q, k, v, causal=causal, variant=self.variant, w4_grid=16)
 
     def last_path(self):
         from flash_attention_cute_amd import _debug
 
-        return _debug.last_path(debug=self.variant != "w4")
+        return _debug.last_path(debug=self.variant not in ("w4", "w4hp"))
 
 
-@pytest.fixture(params=["w4", "p8"])
+@pytest.fixture(params=["w4", "w4hp", "p8"])
 def op(device, request):
     from flash_attention_cute_amd import _debug
     from flash_attention_cute_amd import flash_attention as fam
@@ -47,11 +48,14 @@ def op(device, request):
     # 16 workgroups: each walks 4 Q blocks (3 block switches); the product kernel, and the paired
     # 8-wave variant of the debug library
     _debug.set_knobs(w4_grid=16)
+    if request.param == "w4hp":  # (g = 4: every causal launch below runs head-packed blocks)
+        _debug.set_head_pack(2)
     try:
         yield _Op(request.param)
     finally:
         _debug.set_knobs()
-        if request.param != "w4":
+        _debug.set_head_pack()
+        if request.param == "p8":
             _debug.set_knobs(debug=True)
 
 
@@ -64,6 +68,10 @@ def test_seed_sweep_every_row(op, device, dtype, causal):
         out = op(qd, kd, vd, causal=causal)
         again = op(qd, kd, vd, causal=causal)
         torch.cuda.synchronize()
-        assert op.last_path() == op.variant
+        assert op.last_path() == ("w4" if op.variant == "w4hp" else op.variant)
+        if op.variant == "w4hp" and causal:
+            from flash_attention_cute_amd import _debug
+
+            assert _debug.last_layout() == "headpack"
         assert torch.equal(out, again), f"seed {seed}: two launches differ"
         check(out, q, k, v, 128 ** -0.5, causal, dtype)
