@@ -87,7 +87,7 @@ def test_traffic_absent_without_a_pmc_file(tmp_path, monkeypatch, tiny_libs):
 def test_committed_pmc_files_carry_a_library_hash():
     for p in sorted((ROOT / "profiles").glob("pmc_*.json")):
         d = json.loads(p.read_text())
-        assert len(d.get("lib_sha16", "")) == 16 and len(d.get("code_sha16", "0" * 16)) == 16, p.name
+        assert len(d.get("lib_sha16", "")) == 16 and len(d.get("code_sha16", "")) == 16, p.name
         assert d["hbm_bytes_per_launch"] > 0, p.name
 
 
