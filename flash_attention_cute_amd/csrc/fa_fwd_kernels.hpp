@@ -1005,8 +1005,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // the XCD, snake-ordered (odd rounds reversed) so that a heavy-first causal order balances
     // without a work queue. The next block's Q fragments and first K tile are fetched while the
     // current block drains its pipeline and stores O.
-    // Head-packed blocks (xa.head_pack, dense causal GQA with a multiple of 4 q-heads per kv-head,
-    // multi-round grids): a block is (batch, 4 consecutive q-heads of one kv group, 64-row q-tile),
+    // Head-packed blocks (xa.head_pack, causal GQA with a multiple of 4 q-heads per kv-head, multi-round
+    // grids; dense, RoPE or per-sequence ranges, no window): a block is (batch, 4 consecutive q-heads of one kv group, 64-row q-tile),
     // wave w runs q-head 4 u + w on those 64 rows (block A the first 32, block B the next 32). Every
     // row keeps its own 32-row group and tile order, so the output is the plain layout's bit for bit;
     // but the causal diagonal of a block is ONE tile instead of four (plain 256-row blocks: 4 masked

@@ -736,6 +736,56 @@ def test_head_packed_blocks(device, shape, dtype):
     check(out, q, k, v, d ** -0.5, True, dtype)
 
 
+@pytest.mark.parametrize("entry", ["rope", "varlen", "padded"])
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16], ids=["f16", "bf16"])
+def test_head_packed_blocks_on_rope_and_ranges(device, entry, dtype):
+    """Head-packed blocks on the other causal entries that carry GQA prefill: the fused-RoPE launch
+    (the patched Llama layer's call), packed varlen and padded batches in place (ragged and empty
+    sequences, Sq < Sk). Knob 2 against knob 0: bit-identical; and against the oracle."""
+    from flash_attention_cute_amd import _debug, flash_attn_padded_func, flash_attn_rope_func, flash_attn_varlen_func
+    from tests.test_padded import check_padded, make_batch, oracle_padded, ranges
+    from tests.test_rope import oracle_rope, tables
+    from tests.test_varlen import check_varlen, pack
+
+    seed = zlib.crc32(repr((entry, str(dtype), "hp")).encode())
+    dv = lambda t: t.to(device)  # noqa: E731
+    if entry == "rope":
+        b, hq, hkv, s, d = 2, 8, 2, 700, 128
+        q, k, v = make_batch(b, hq, hkv, s, s, d, dtype, seed, "bshd")  # HF projection views
+        cos, sin = tables(b, s, d, dtype, seed)
+        args = tuple(map(dv, (q, k, v, cos, sin)))
+        run = lambda: flash_attn_rope_func(*args, causal=True)  # noqa: E731
+        ref = lambda out: check(out, oracle_rope(q, cos, sin), k, v, d ** -0.5, True, dtype)  # noqa: E731
+    elif entry == "varlen":
+        case = (8, 2, 128, [(700, 700), (130, 130), (0, 0), (45, 300), (300, 300), (64, 64)])
+        q, k, v, cu_q, cu_k, mq, mk = pack(case, dtype, seed)
+        args = tuple(map(dv, (q, k, v, cu_q, cu_k)))
+        run = lambda: flash_attn_varlen_func(*args, mq, mk, causal=True)  # noqa: E731
+        ref = lambda out: check_varlen(out, q, k, v, cu_q, cu_k, 128 ** -0.5, True, dtype)  # noqa: E731
+    else:
+        b, hq, hkv, sq, sk, d = 4, 8, 2, 600, 700, 128
+        q, k, v = make_batch(b, hq, hkv, sq, sk, d, dtype, seed, "bshd")
+        rg = ranges(b, sq, sk, seed, "mixed")
+        args = tuple(map(dv, (q, k, v) + rg))
+        run = lambda: flash_attn_padded_func(*args, causal=True)  # noqa: E731
+        ref = lambda out: check_padded(out, oracle_padded(q, k, v, *rg, d ** -0.5, True), dtype)  # noqa: E731
+    _debug.set_knobs()
+    try:
+        _debug.set_head_pack(2)
+        out = run()
+        assert _debug.last_path() == "w4" and _debug.last_layout() == "headpack"
+        with _debug.knobs(w4_grid=8):
+            small = run()
+        _debug.set_head_pack(0)
+        plain = run()
+        assert _debug.last_layout() != "headpack"
+        torch.cuda.synchronize()
+    finally:
+        _debug.set_head_pack()
+    assert torch.equal(out, plain) and torch.equal(out, small)
+    ref(out)
+
+
 def test_head_packed_blocks_by_default(device):
     """The default rule: multi-round causal grids with g = 4 take head-packed blocks (C4 / C5's class);
     g = 8 too (two q-head quads per kv group); g = 2, non-causal, and one-round grids (zigzag /
@@ -749,6 +799,11 @@ def test_head_packed_blocks_by_default(device):
     m.flash_attn_func(*big, causal=True)
     assert _debug.last_layout() == "headpack"
     m.flash_attn_func(*big, causal=False)
+    assert _debug.last_layout() == "plain"
+    cs = torch.randn(2, 2048, 128, device=device, dtype=torch.float16)
+    m.flash_attn_rope_func(*big, cs, cs, causal=True)  # the patched Llama layer's launch
+    assert _debug.last_layout() == "headpack"
+    m.flash_attn_window_func(*big, 1000, causal=True)  # (not the local window)
     assert _debug.last_layout() == "plain"
     g2 = [torch.randn(2, h, 2048, 128, device=device, dtype=torch.float16) for h in (32, 16, 16)]
     m.flash_attn_func(*g2, causal=True)
