@@ -1006,7 +1006,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     // without a work queue. The next block's Q fragments and first K tile are fetched while the
     // current block drains its pipeline and stores O.
     // Head-packed blocks (xa.head_pack, causal GQA with a multiple of 4 q-heads per kv-head, multi-round
-    // grids; dense, RoPE or per-sequence ranges, no window): a block is (batch, 4 consecutive q-heads of one kv group, 64-row q-tile),
+    // grids; dense, RoPE, per-sequence ranges, local window): a block is (batch, 4 consecutive q-heads of one kv group, 64-row q-tile),
     // wave w runs q-head 4 u + w on those 64 rows (block A the first 32, block B the next 32). Every
     // row keeps its own 32-row group and tile order, so the output is the plain layout's bit for bit;
     // but the causal diagonal of a block is ONE tile instead of four (plain 256-row blocks: 4 masked
@@ -1175,7 +1175,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         j_lo = j_um = 0;
         if (wl >= 0) {
             const int lo0 = m0 + diag - wl;                         // the first row's first key
-            const int lo1 = min(m0 + kBlockM, Sq) - 1 + diag - wl;  // the last row's
+            const int lo1 = min(m0 + (hp ? 64 : kBlockM), Sq) - 1 + diag - wl;  // the last row's
             j_lo = min(max(lo0, 0) / kBlockN, n_end);
             j_um = min((max(lo1, 0) + kBlockN - 1) / kBlockN, n_end);
         }

@@ -736,13 +736,15 @@ def test_head_packed_blocks(device, shape, dtype):
     check(out, q, k, v, d ** -0.5, True, dtype)
 
 
-@pytest.mark.parametrize("entry", ["rope", "varlen", "padded"])
+@pytest.mark.parametrize("entry", ["rope", "varlen", "padded", "window63", "window300", "window0", "varlen_window"])
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16], ids=["f16", "bf16"])
-def test_head_packed_blocks_on_rope_and_ranges(device, entry, dtype):
+def test_head_packed_blocks_on_rope_ranges_and_window(device, entry, dtype):
     """Head-packed blocks on the other causal entries that carry GQA prefill: the fused-RoPE launch
     (the patched Llama layer's call), packed varlen and padded batches in place (ragged and empty
-    sequences, Sq < Sk). Knob 2 against knob 0: bit-identical; and against the oracle."""
-    from flash_attention_cute_amd import _debug, flash_attn_padded_func, flash_attn_rope_func, flash_attn_varlen_func
+    sequences, Sq < Sk), the local window (narrower than, one less than and wider than a 64-key tile)
+    alone and per packed sequence. Knob 2 against knob 0: bit-identical; and against the oracle."""
+    from flash_attention_cute_amd import (_debug, flash_attn_padded_func, flash_attn_rope_func, flash_attn_varlen_func,
+                                          flash_attn_window_func)
     from tests.test_padded import check_padded, make_batch, oracle_padded, ranges
     from tests.test_rope import oracle_rope, tables
     from tests.test_varlen import check_varlen, pack
@@ -762,6 +764,29 @@ def test_head_packed_blocks_on_rope_and_ranges(device, entry, dtype):
         args = tuple(map(dv, (q, k, v, cu_q, cu_k)))
         run = lambda: flash_attn_varlen_func(*args, mq, mk, causal=True)  # noqa: E731
         ref = lambda out: check_varlen(out, q, k, v, cu_q, cu_k, 128 ** -0.5, True, dtype)  # noqa: E731
+    elif entry.startswith("window"):
+        wl = int(entry[6:])
+        b, hq, hkv, sq, sk, d = 2, 8, 2, 1000, 1100, 128
+        q, k, v = make(b, hq, hkv, sq, sk, d, dtype, seed)
+        args = tuple(map(dv, (q, k, v)))
+        run = lambda: flash_attn_window_func(*args, wl, causal=True)  # noqa: E731
+
+        def ref(out):
+            r = OC.forward(q, k, v, d ** -0.5, True, window_left=wl).float()
+            err = (out.float().cpu() - r).abs()
+            tol = TOL[dtype][0]
+            assert bool((err <= tol + tol * r.abs()).all()), f"max err {err.max().item():.3e}"
+    elif entry == "varlen_window":
+        case = (8, 2, 128, [(700, 700), (130, 130), (0, 0), (45, 300), (300, 300), (64, 64)])
+        q, k, v, cu_q, cu_k, mq, mk = pack(case, dtype, seed)
+        args = tuple(map(dv, (q, k, v, cu_q, cu_k)))
+        run = lambda: flash_attn_varlen_func(*args, mq, mk, causal=True, window_left=100)  # noqa: E731
+
+        def ref(out):
+            r = OC.forward_varlen(q, k, v, cu_q, cu_k, 128 ** -0.5, True, window_left=100).float()
+            err = (out.float().cpu() - r).abs()
+            tol = TOL[dtype][0]
+            assert bool((err <= tol + tol * r.abs()).all()), f"max err {err.max().item():.3e}"
     else:
         b, hq, hkv, sq, sk, d = 4, 8, 2, 600, 700, 128
         q, k, v = make_batch(b, hq, hkv, sq, sk, d, dtype, seed, "bshd")
@@ -803,8 +828,8 @@ def test_head_packed_blocks_by_default(device):
     cs = torch.randn(2, 2048, 128, device=device, dtype=torch.float16)
     m.flash_attn_rope_func(*big, cs, cs, causal=True)  # the patched Llama layer's launch
     assert _debug.last_layout() == "headpack"
-    m.flash_attn_window_func(*big, 1000, causal=True)  # (not the local window)
-    assert _debug.last_layout() == "plain"
+    m.flash_attn_window_func(*big, 1000, causal=True)  # the local window too
+    assert _debug.last_layout() == "headpack"
     g2 = [torch.randn(2, h, 2048, 128, device=device, dtype=torch.float16) for h in (32, 16, 16)]
     m.flash_attn_func(*g2, causal=True)
     assert _debug.last_layout() != "headpack"
