@@ -2,8 +2,9 @@
 
 * the golden vectors the REFERENCE's own operator produced (tests/golden/make_golden.py, reference
   flash_attention/flash_attention.py CPU path) run through the HIP kernel directly;
-* C2 / C3 / C4 at full size: 8 sampled (batch, q-head) pairs per config -- first, last, and heads
-  from a middle kv group -- against the oracle, every head against size-independent properties;
+* C2 / C3 / C4 at full size: the whole output tensor, every (batch, q-head), against the C oracle,
+  plus size-independent properties;
+* head-packed blocks against the reference's fixtures directly;
 * the bf16 bar of BASELINE.md (C3, C5): the kernel's error against fp32 must stay within 2x the
   error torch's bf16 SDPA shows against fp32 on the same inputs, measured in the same run;
 * C5 as BASELINE.json states it: the patched ``LlamaAttention.forward`` at Llama-3-8B dims
@@ -199,6 +200,61 @@ def test_reference_golden_pairs_on_gpu(op, device, fname):
     assert (err <= tol + tol * ref.abs()).all(), err.max().item()
     assert err.mean().item() < tol / 8
     assert m.split_errors() == 0
+
+
+def test_reference_golden_vectors_head_packed(op, device):
+    """Head-packed blocks pinned to the REFERENCE's outputs directly (not only bit-equal to the plain
+    layout): every causal fixture with a multiple of 4 q-heads per kv-head and more than one 64-row
+    q-tile (golden_gqa, golden_gqa128 and both pairs fixtures, whose default layouts are plain or
+    key-split) forced into head-packed blocks, the fixtures' own tolerances."""
+    import sys
+
+    from flash_attention_cute_amd import _debug
+
+    sys.path.insert(0, str(GOLD))
+    from make_golden import pairs_codes
+
+    meta = json.loads((GOLD / "golden_meta.json").read_text())
+    tols = {"f16": 2e-3, "bf16": 1.6e-2}
+    cases = []  # (q, k, v, ref, dtype, pick)
+    for fname, key in (("golden_gqa.npz", "n_gqa_cases"), ("golden_gqa128.npz", "n_gqa128_cases")):
+        g = np.load(GOLD / fname)
+        cs = float(g["code_scale"])
+        for i in range(meta[key]):
+            b, hq, hkv, sq, sk, d, causal = (int(x) for x in g[f"case{i}_meta"])
+            if not causal or (hq // hkv) % 4 or sq <= 64:
+                continue
+            dtype = str(g[f"case{i}_dtype"])
+            tdt = torch.float16 if dtype == "f16" else torch.bfloat16
+            q, k, v = (torch.from_numpy(g[f"case{i}_{n_}c"]).to(tdt).div_(cs) for n_ in "qkv")
+            cases.append((q, k, v, _gold_tensor(g[f"case{i}_o"], dtype), dtype, None))
+    for fname in meta["pairs_files"]:
+        g = np.load(GOLD / fname)
+        b, hq, hkv, sq, sk, d, causal = (int(x) for x in g["meta"])
+        dtype = str(g["dtype"])
+        tdt = torch.float16 if dtype == "f16" else torch.bfloat16
+        q, k, v = (torch.from_numpy(c).to(tdt).div_(float(g["code_scale"]))
+                   for c in pairs_codes(int(g["seed"]), b, hq, hkv, sq, sk, d))
+        cases.append((q, k, v, _gold_tensor(g["o"], dtype), dtype,
+                      (torch.from_numpy(g["heads"]), torch.from_numpy(g["rows"]))))
+    assert len(cases) == 5  # gqa case 0 (D 64), gqa128 cases 0 and 1, the two pairs fixtures
+    _debug.set_knobs()
+    try:
+        _debug.set_head_pack(2)
+        _debug.set_split(0)
+        for n, (q, k, v, ref, dtype, pick) in enumerate(cases):
+            out = op(q.to(device), k.to(device), v.to(device), causal=True)
+            assert _debug.last_layout() == "headpack", n
+            out = out.float().cpu()
+            if pick is not None:
+                out = out[:, pick[0]][:, :, pick[1]]
+            err = (out - ref.float()).abs()
+            tol = tols[dtype]
+            assert (err <= tol + tol * ref.float().abs()).all(), (n, err.max().item())
+            assert err.mean().item() < tol / 8, (n, err.mean().item())
+    finally:
+        _debug.set_head_pack()
+        _debug.set_split()
 
 
 @pytest.mark.parametrize("causal", [False, True])
