@@ -151,19 +151,27 @@ def last_dec_fused(debug: bool = False) -> bool:
 
 def set_head_pack(mode: int | None = None, debug: bool = False) -> None:
     """Head-packed causal GQA blocks (4 q-heads per kv-head, one per wave, 64 rows; fa_launch.h
-    use_head_pack): 0 never, 1 on multi-round grids (the default), 2 wherever they apply; None restores it."""
+    use_head_pack, use_head_pack_split): 0 never, 1 on multi-round grids and for key-split pieces (the
+    default), 2 wherever they apply; None restores it."""
     lib(debug).fa_debug_set_head_pack(-1 if mode is None else int(mode))
 
 
 def last_layout(debug: bool = False) -> str:
     """Causal block layout of the last prefill launch on this thread: "plain", "zigzag", "split"
-    (key-split, as halves or as pairs: last_split_pairs) or "headpack"."""
-    return {0: "plain", 1: "zigzag", 2: "split", 3: "split", 4: "headpack"}[lib(debug).fa_debug_last_zigzag()]
+    (key-split, as halves or as pairs: last_split_pairs; over head-packed blocks: last_head_pack) or
+    "headpack"."""
+    return {0: "plain", 1: "zigzag", 2: "split", 3: "split", 4: "headpack", 5: "split",
+            6: "split"}[lib(debug).fa_debug_last_zigzag()]
 
 
 def last_split_pairs(debug: bool = False) -> bool:
     """Whether the last prefill launch on this thread laid its key-split pieces out as pairs."""
-    return lib(debug).fa_debug_last_zigzag() == 3
+    return lib(debug).fa_debug_last_zigzag() in (3, 6)
+
+
+def last_head_pack(debug: bool = False) -> bool:
+    """Whether the last prefill launch on this thread ran head-packed blocks (key-split pieces or not)."""
+    return lib(debug).fa_debug_last_zigzag() in (4, 5, 6)
 
 
 def forward(q, k, v, softmax_scale=None, causal=False, variant="w8", window_left=-1, w4_grid=None,

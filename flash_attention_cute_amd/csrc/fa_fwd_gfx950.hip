@@ -137,7 +137,8 @@ extern "C" void fa_debug_set_head_pack(int mode) {
 }
 // zigzag knob (fa_launch.h Knobs::zigzag): 0 never, 1 when the blocks fit one round, 2 always; < 0
 // restores the environment / default value. fa_debug_last_zigzag: the causal block layout of the
-// last prefill launch on this thread: 0 plain, 1 zigzag, 2 key-split, 3 key-split pairs, 4 head-packed.
+// last prefill launch on this thread: 0 plain, 1 zigzag, 2 key-split, 3 key-split pairs, 4 head-packed,
+// 5 / 6 key-split halves / pairs over head-packed blocks.
 extern "C" void fa_debug_set_zigzag(int mode) {
     knobs_mut().zigzag = mode < 0 ? env_defaults().zigzag : mode;
 }

@@ -1028,19 +1028,18 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
     const bool spl = kCausal && xa.split_ws != nullptr;
     const bool pairs = spl && xa.split_pairs != 0;
     const int nqp = n_qtiles >> 1;  // (key-split launches: the host passes twice the plain q-tiles)
-    const uint32_t nunits = pairs ? (uint32_t)((nqp + 1) >> 1) * p.num_heads_q * p.batch_size : spl ? nwg >> 1 : nwg;
+    const uint32_t nunits = pairs ? (uint32_t)((nqp + 1) >> 1) * (uint32_t)heads_u * p.batch_size : spl ? nwg >> 1 : nwg;
     const uint32_t nux = (nunits - xcd + 7) >> 3;  // units of this XCD
     const uint32_t cnt = pairs ? 2 * gx : spl ? 2 * nux : (nwg - xcd + 7) >> 3;  // Q blocks of this XCD
     auto nend_of = [&](const int t) __attribute__((always_inline)) {  // a dense causal q-tile's key tiles
-        const int x = diag + min((t + 1) * kBlockM, Sq);
+        const int x = diag + min((t + 1) * (hp ? 64 : kBlockM), Sq);
         return min(x <= 0 ? 0 : (x + kBlockN - 1) / kBlockN, n_blocks);
     };
     // pairs: item k = rnd * gx + c of workgroup c; false if it has none
     auto pair_item = [&](const uint32_t k, Work &w) __attribute__((always_inline)) {
         const uint32_t r = k >= gx ? 1u : 0u, c = k - r * gx;
         if (c >= 2 * nux) return false;
-        w = decode_work<kCausal>(nunits, xcd + 8 * (c >> 1), (nqp + 1) >> 1, (int)p.num_heads_q,
-                                 (int)p.head_q_per_group);
+        w = decode_work<kCausal>(nunits, xcd + 8 * (c >> 1), (nqp + 1) >> 1, heads_u, grp_u);
         const int pl = w.qtile, hv = nqp - 1 - pl;  // light and heavy q-tile (equal: the middle one)
         const int ch = nend_of(hv);
         const int mid = hv == pl ? ch >> 1 : max(0, ((ch - nend_of(pl)) >> 1) - FA_PAIR_SHIFT);
@@ -1067,7 +1066,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
         if (pairs) {
             pair_item(k, w);
         } else {
-            w = decode_work<kCausal>(nunits, xcd + 8 * (k >> 1), nqp, (int)p.num_heads_q, (int)p.head_q_per_group);
+            w = decode_work<kCausal>(nunits, xcd + 8 * (k >> 1), nqp, heads_u, grp_u);
             w.kr = (k & 1 ? 2 : 1) | ((nend_of(w.qtile) >> 1) << 2);  // piece k & 1 of the halves
         }
         // (wave-uniform: said so, or the block's buffer descriptors may land in VGPRs, which the
@@ -1188,7 +1187,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_w4(const fa_fwd_params p, const
             n_end = kind == 1 ? mid : n_end;
             n_pipe = min(n_pipe, n_end);
             blk_split = kind != 0;
-            split_slot = (b * (int)p.num_heads_q + hq) * nqp + wk.qtile;
+            split_slot = (b * heads_u + wk.hq) * nqp + wk.qtile;  // (hp: wk.hq is the quad, one record per wave)
         }
     };
     set_block(work_of(kblk));
@@ -2479,15 +2478,18 @@ int launch_one(const fa_fwd_params &p, const PathArgs &xa, hipStream_t stream) {
     PathArgs xz = xa;
     if (variant == 1) xz.split_ws = nullptr;
     // (the default rules are disjoint: head-packed blocks on multi-round grids, zigzag on one-round ones;
-    // the head_pack knob 2 forces them over zigzag)
-    xz.head_pack = !xz.split_ws && variant != 1 && use_head_pack(p, C, xa) ? 1 : 0;
+    // the head_pack knob 2 forces them over zigzag; key-split pieces are head-packed wherever the layout
+    // applies, use_head_pack_split)
+    xz.head_pack = variant != 1 && (xz.split_ws ? use_head_pack_split(p, C, xa) : use_head_pack(p, C, xa)) ? 1 : 0;
     xz.zigzag = !xz.split_ws && !xz.head_pack && variant != 1 && use_zigzag(p, C, xa) ? 1 : 0;
-    const int64_t n_plain = (p.seqlen_q + kBlockM - 1) / kBlockM;
-    xz.split_pairs = xz.split_ws && use_split_pairs(p, device_cus()) ? 1 : 0;
-    const int64_t n_pairs = (n_plain + 1) / 2 * p.num_heads_q * p.batch_size;
-    const int64_t n_qtiles = xz.split_ws ? 2 * n_plain : xz.zigzag ? zigzag_qtiles(p.seqlen_q)
-                           : xz.head_pack ? (p.seqlen_q + 63) / 64 : n_plain;
-    const int64_t nwg = n_qtiles * (xz.head_pack ? p.num_heads_q / 4 : p.num_heads_q) * p.batch_size;
+    // q-tiles per (batch, q-head) or, head-packed, per (batch, q-head quad): 256 or 64 rows
+    const int64_t n_plain = xz.head_pack ? (p.seqlen_q + 63) / 64 : (p.seqlen_q + kBlockM - 1) / kBlockM;
+    const int64_t heads_u = xz.head_pack ? p.num_heads_q / 4 : p.num_heads_q;
+    xz.split_pairs = xz.split_ws && use_split_pairs(n_plain * heads_u * p.batch_size, heads_u * p.batch_size,
+                                                    device_cus()) ? 1 : 0;
+    const int64_t n_pairs = (n_plain + 1) / 2 * heads_u * p.batch_size;
+    const int64_t n_qtiles = xz.split_ws ? 2 * n_plain : xz.zigzag ? zigzag_qtiles(p.seqlen_q) : n_plain;
+    const int64_t nwg = n_qtiles * heads_u * p.batch_size;
 #ifdef FA_DEBUG_VARIANTS
     if (variant == 1)
         hipLaunchKernelGGL((fa_fwd_w8<DT, C, kD, kExact>), dim3((uint32_t)nwg), dim3(kThreads), 0, stream, p,
@@ -2502,7 +2504,7 @@ int launch_one(const fa_fwd_params &p, const PathArgs &xa, hipStream_t stream) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(FA_ERR_LAUNCH, "HIP launch failed: %s", hipGetErrorString(e));
     set_last_path(variant == 1 ? kPathW8 : variant == 2 ? kPathW4Slow : kPathW4);
-    set_last_zigzag(xz.split_ws ? 2 + xz.split_pairs : xz.head_pack ? 4 : xz.zigzag);
+    set_last_zigzag(xz.split_ws ? (xz.head_pack ? 5 : 2) + xz.split_pairs : xz.head_pack ? 4 : xz.zigzag);
     return FA_OK;
 }
 

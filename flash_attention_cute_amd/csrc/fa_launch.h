@@ -165,6 +165,16 @@ inline bool use_head_pack(const fa_fwd_params &p, bool causal, const PathArgs &x
     return nwg > device_cus();
 }
 
+// Head-packed key-split pieces (fa_fwd_w4 "Head-packed blocks" + "key-split blocks"): a key-split
+// launch (one-round grid, use_split) with a multiple of 4 q-heads per kv-head runs its pieces over
+// (batch, q-head quad, 64-row q-tile) blocks -- the halves or pairs layout over those units, the same
+// hand-off per (block, wave) (each wave one q-head's 64 rows, as a plain block's wave) -- so a piece's
+// diagonal is one tile. Knob head_pack: 0 never, 1 and 2 wherever this applies.
+inline bool use_head_pack_split(const fa_fwd_params &p, bool causal, const PathArgs &xa) {
+    return causal && !xa.k_rng && !xa.cos && xa.window_left < 0 && knobs().head_pack != 0 &&
+           p.head_q_per_group % 4 == 0 && p.seqlen_q > 64;
+}
+
 // Key-split causal blocks: dense causal launches (no varlen, window or RoPE) when the caller passes
 // the workspace. Knob 1 (default): where measured faster than zigzag (profiles/r4_split_sweep.log,
 // same-process A/B): the plain blocks fit one round of the grid and the keys are long enough for
@@ -201,10 +211,12 @@ inline int64_t split_wave_floats(int64_t headdim) {
 // two workgroups per unit of its list when that fits the grid cap (units are dealt to XCDs, so 2 *
 // units workgroups could leave some XCD short and run both pieces of a block on one workgroup)
 int64_t w4_grid_split(int64_t units);
-inline bool use_split_pairs(const fa_fwd_params &p, int64_t cus) {
+// blocks: the launch's unsplit Q blocks (q-tiles x rows of the work order); rows: its (batch, q-head)
+// or, head-packed, (batch, q-head quad) rows
+inline bool use_split_pairs(int64_t blocks, int64_t rows, int64_t cus) {
     if (knobs().split_pairs == 0) return false;
-    const int64_t nq = (p.seqlen_q + kBlockM - 1) / kBlockM, units = (nq + 1) / 2 * p.num_heads_q * p.batch_size;
-    return 2 * nq * p.num_heads_q * p.batch_size > cus && w4_grid_split(units) == 16 * ((units + 7) / 8);
+    const int64_t nq = blocks / rows, units = (nq + 1) / 2 * rows;
+    return 2 * blocks > cus && w4_grid_split(units) == 16 * ((units + 7) / 8);
 }
 inline int64_t split_blocks(const fa_fwd_params &p) {
     return (p.seqlen_q + kBlockM - 1) / kBlockM * p.num_heads_q * p.batch_size;

@@ -460,7 +460,8 @@ def test_key_split_pairs(device, shape):
 
 
 def test_key_split_pairs_by_default_on_the_c4_share(device):
-    """The default rule sends C4's 8-way share (B1 Hq16 Hkv4 S4096 causal) to key-split pairs."""
+    """The default rule sends C4's 8-way share (B1 Hq16 Hkv4 S4096 causal) to key-split pairs over
+    head-packed blocks."""
     import flash_attention_cute_amd as m
     from flash_attention_cute_amd import _debug
 
@@ -468,8 +469,63 @@ def test_key_split_pairs_by_default_on_the_c4_share(device):
     _debug.set_knobs()
     _debug.set_split()
     _debug.set_split_pairs()
+    _debug.set_head_pack()
     m.flash_attn_func(q, k, v, causal=True)
-    assert _debug.last_layout() == "split" and _debug.last_split_pairs()
+    assert _debug.last_layout() == "split" and _debug.last_split_pairs() and _debug.last_head_pack()
+
+
+HP_SPLIT = [  # (B, Hq, Hkv, Sq, Sk, D): one-round causal GQA grids, g % 4 == 0
+    (1, 16, 4, 4096, 4096, 128),  # C4's 8-way share: pairs over 64 q-tiles of 4 quads
+    (1, 8, 2, 1024, 1024, 128),   # halves (16 q-tiles x 2 quads x 2 pieces)
+    (1, 32, 8, 1280, 2000, 128),  # Sq < Sk
+    (2, 8, 1, 1500, 700, 64),     # Sq > Sk: the first rows see no key (output 0); g = 8, D = 64
+    (1, 4, 1, 300, 300, 128),     # ragged: a 44-row last q-tile
+]
+
+
+@pytest.mark.parametrize("shape", HP_SPLIT, ids=[str(s) for s in HP_SPLIT])
+@pytest.mark.parametrize("pairs", [1, 0], ids=["pairs", "halves"])
+def test_head_packed_key_split(device, shape, pairs):
+    """Key-split pieces over head-packed blocks (fa_launch.h use_head_pack_split: the halves or pairs
+    layout over (batch, q-head quad, 64-row q-tile) units, one hand-off per (block, wave)): against the
+    oracle, two launches and a capped persistent grid bit-identical, no hand-off error, close to the
+    plain-block key-split layout (different split points: summation order only)."""
+    import flash_attention_cute_amd as m
+    from flash_attention_cute_amd import _debug
+
+    b, hq, hkv, sq, sk, d = shape
+    dtype = torch.bfloat16 if pairs else torch.float16
+    q, k, v = make(b, hq, hkv, sq, sk, d, dtype, zlib.crc32(repr((shape, pairs, "hpsplit")).encode()))
+    qd, kd, vd = q.to(device), k.to(device), v.to(device)
+    _debug.set_knobs()
+    _debug.set_split(2)
+    _debug.set_split_pairs(pairs)
+    _debug.set_head_pack()
+    m.split_errors(reset=True)
+    try:
+        out = m.flash_attn_func(qd, kd, vd, causal=True)
+        assert _debug.last_layout() == "split" and _debug.last_head_pack()
+        layout_pairs = _debug.last_split_pairs()
+        again = m.flash_attn_func(qd, kd, vd, causal=True)
+        with _debug.knobs(w4_grid=16):  # many rounds per workgroup: the halves, pieces in every order
+            small = m.flash_attn_func(qd, kd, vd, causal=True)
+            assert _debug.last_head_pack() and not _debug.last_split_pairs()
+        _debug.set_head_pack(0)
+        plain = m.flash_attn_func(qd, kd, vd, causal=True)
+        assert _debug.last_layout() == "split" and not _debug.last_head_pack()
+        torch.cuda.synchronize()
+    finally:
+        _debug.set_split()
+        _debug.set_split_pairs()
+        _debug.set_head_pack()
+    assert m.split_errors() == 0
+    assert torch.equal(out, again)
+    if not layout_pairs:
+        assert torch.equal(out, small)
+    check(out, q, k, v, d ** -0.5, True, dtype)
+    check(small, q, k, v, d ** -0.5, True, dtype)
+    tol = 4e-3 if dtype == torch.float16 else 3e-2
+    assert (out.float() - plain.float()).abs().max().item() < tol
 
 
 def test_key_split_only_with_a_workspace(device):
@@ -553,29 +609,32 @@ def test_key_split_under_graph_capture(device):
     assert m.split_errors() == 0
 
 
-@pytest.mark.parametrize("layout", ["halves", "pairs"])
+@pytest.mark.parametrize("layout", ["halves", "pairs", "halves_hp", "pairs_hp"])
 def test_key_split_timeout_leaves_the_next_launch_correct(device, layout):
     """A hand-off that times out (debug library: wave 0 of the last q-tile of (batch 0, q-head 0) holds
     its ready mark until its partner has abandoned the pair) is counted exactly once, and the NEXT
     launches on the same stream are correct against the oracle with no further error: the abandoned
     pair's arrivals word was left 0, so no launch inherits a stale ready mark (fa_fwd_w4 key-split
-    hand-off). Reference behaviour kept by the good launches: plain blocks, template.cuh:516-563."""
+    hand-off). Both layouts, over plain and head-packed blocks (_hp: 64-row q-tiles of q-head quads).
+    Reference behaviour kept by the good launches: plain blocks, template.cuh:516-563."""
     from flash_attention_cute_amd import _debug
 
-    shape = (1, 4, 2, 1024, 1024, 128) if layout == "halves" else (1, 16, 4, 4096, 4096, 128)
+    pairs, hp = layout.startswith("pairs"), layout.endswith("_hp")
+    shape = (1, 16, 4, 4096, 4096, 128) if pairs else (1, 8, 2, 1024, 1024, 128)
     b, hq, hkv, sq, sk, d = shape
     dtype = torch.float16
     q, k, v = make(b, hq, hkv, sq, sk, d, dtype, zlib.crc32(repr((shape, "fault")).encode()))
     qd, kd, vd = q.to(device), k.to(device), v.to(device)
     dl = _debug.lib(debug=True)
     _debug.set_split(2, debug=True)
-    _debug.set_split_pairs(1 if layout == "pairs" else 0, debug=True)
+    _debug.set_split_pairs(1 if pairs else 0, debug=True)
+    _debug.set_head_pack(1 if hp else 0, debug=True)
     dl.fa_split_errors(1)
     try:
         _debug.set_split_fault(True)
         bad = _debug.forward(qd, kd, vd, causal=True, variant="w4", workspace=True)
         assert _debug.last_path(debug=True) == "w4" and _debug.last_layout(debug=True) == "split"
-        assert (dl.fa_debug_last_zigzag() == 3) == (layout == "pairs")
+        assert _debug.last_split_pairs(debug=True) == pairs and _debug.last_head_pack(debug=True) == hp
         torch.cuda.synchronize()
         assert dl.fa_split_errors(0) == 1
         _debug.set_split_fault(False)
@@ -587,15 +646,18 @@ def test_key_split_timeout_leaves_the_next_launch_correct(device, layout):
         _debug.set_split_fault(False)
         _debug.set_split(debug=True)
         _debug.set_split_pairs(debug=True)
+        _debug.set_head_pack(debug=True)
         _debug.set_knobs(debug=True)
     assert torch.equal(good, again)
     check(good, q, k, v, d ** -0.5, True, dtype)
     # the faulted launch can differ from the good one only in the abandoned block's rows (wave 0 of
-    # q-tile nq - 1 of (batch 0, q-head 0): rows 0-31 and 128-159 of that 256-row block; the partner's
-    # records are usually written by the time it gives up, so they may well be right)
-    nq = (sq + 255) // 256
+    # q-tile nq - 1 of (batch 0, q-head 0): rows 0-31 and 128-159 of that 256-row block, or head-packed
+    # all 64 rows of that 64-row q-tile; the partner's records are usually written by the time it gives
+    # up, so they may well be right)
+    rows = 64 if hp else 256
+    nq = (sq + rows - 1) // rows
     for bb, hh, m in (bad.float() != good.float()).any(dim=-1).nonzero().tolist():
-        assert (bb, hh) == (0, 0) and m // 256 == nq - 1 and (m % 256) % 128 < 32, (bb, hh, m)
+        assert (bb, hh) == (0, 0) and m // rows == nq - 1 and (hp or (m % 256) % 128 < 32), (bb, hh, m)
 
 
 def test_split_layouts_need_same_xcd_placement(device):

@@ -6,8 +6,9 @@ launches of the same inputs. DESIGN.md section 5 records one discarded experimen
 524k differed; this sweep checks ~0.8M rows of the kept kernel (fa_fwd_w4, persistent, several Q
 blocks per workgroup through a capped grid so every block switch -- Q staged by LDS-DMA, the
 first-tile rescale -- runs many times) and requires every row within the parity tolerance and two
-launches bit-identical. The same sweep runs the head-packed causal layout (forced) and the paired
-8-wave variant fa_fwd_p8.
+launches bit-identical. The same sweep runs the head-packed causal layout (forced), key-split pieces
+over head-packed blocks (forced split: the halves across many rounds, every hand-off order) and the
+paired 8-wave variant fa_fwd_p8.
 """
 from __future__ import annotations
 
@@ -29,17 +30,18 @@ class _Op:
         from flash_attention_cute_amd import _debug
         from flash_attention_cute_amd import flash_attn_func
 
-        if self.variant in ("w4", "w4hp"):  # the product op (w4hp: head-packed causal blocks forced)
+        if self.variant in ("w4", "w4hp", "w4hpsplit"):  # the product op (w4hp: head-packed causal blocks
+            # forced; w4hpsplit: key-split forced, its pieces head-packed)
             return flash_attn_func(q, k, v, causal=causal)
         return _debug.forward(q, k, v, causal=causal, variant=self.variant, w4_grid=16)
 
     def last_path(self):
         from flash_attention_cute_amd import _debug
 
-        return _debug.last_path(debug=self.variant not in ("w4", "w4hp"))
+        return _debug.last_path(debug=self.variant not in ("w4", "w4hp", "w4hpsplit"))
 
 
-@pytest.fixture(params=["w4", "w4hp", "p8"])
+@pytest.fixture(params=["w4", "w4hp", "w4hpsplit", "p8"])
 def op(device, request):
     from flash_attention_cute_amd import _debug
     from flash_attention_cute_amd import flash_attention as fam
@@ -50,11 +52,19 @@ def op(device, request):
     _debug.set_knobs(w4_grid=16)
     if request.param == "w4hp":  # (g = 4: every causal launch below runs head-packed blocks)
         _debug.set_head_pack(2)
+    if request.param == "w4hpsplit":
+        import flash_attention_cute_amd as m
+
+        _debug.set_split(2)
+        m.split_errors(reset=True)
     try:
         yield _Op(request.param)
+        if request.param == "w4hpsplit":
+            assert m.split_errors() == 0
     finally:
         _debug.set_knobs()
         _debug.set_head_pack()
+        _debug.set_split()
         if request.param == "p8":
             _debug.set_knobs(debug=True)
 
@@ -68,10 +78,11 @@ def test_seed_sweep_every_row(op, device, dtype, causal):
         out = op(qd, kd, vd, causal=causal)
         again = op(qd, kd, vd, causal=causal)
         torch.cuda.synchronize()
-        assert op.last_path() == ("w4" if op.variant == "w4hp" else op.variant)
-        if op.variant == "w4hp" and causal:
+        assert op.last_path() == ("w4" if op.variant.startswith("w4") else op.variant)
+        if op.variant.startswith("w4hp") and causal:
             from flash_attention_cute_amd import _debug
 
-            assert _debug.last_layout() == "headpack"
+            assert _debug.last_head_pack()
+            assert _debug.last_layout() == ("split" if op.variant == "w4hpsplit" else "headpack")
         assert torch.equal(out, again), f"seed {seed}: two launches differ"
         check(out, q, k, v, 128 ** -0.5, causal, dtype)
