@@ -2480,13 +2480,21 @@ int launch_one(const fa_fwd_params &p, const PathArgs &xa, hipStream_t stream) {
     // (the default rules are disjoint: head-packed blocks on multi-round grids, zigzag on one-round ones;
     // the head_pack knob 2 forces them over zigzag; key-split pieces are head-packed wherever the layout
     // applies, use_head_pack_split)
-    xz.head_pack = variant != 1 && (xz.split_ws ? use_head_pack_split(p, C, xa) : use_head_pack(p, C, xa)) ? 1 : 0;
-    xz.zigzag = !xz.split_ws && !xz.head_pack && variant != 1 && use_zigzag(p, C, xa) ? 1 : 0;
     // q-tiles per (batch, q-head) or, head-packed, per (batch, q-head quad): 256 or 64 rows
-    const int64_t n_plain = xz.head_pack ? (p.seqlen_q + 63) / 64 : (p.seqlen_q + kBlockM - 1) / kBlockM;
+    auto qtiles_of = [&](const bool hp) { return hp ? (p.seqlen_q + 63) / 64 : (p.seqlen_q + kBlockM - 1) / kBlockM; };
+    auto rows_of = [&](const bool hp) { return (hp ? p.num_heads_q / 4 : p.num_heads_q) * p.batch_size; };
+    auto pairs_of = [&](const bool hp) { return use_split_pairs(qtiles_of(hp) * rows_of(hp), rows_of(hp), device_cus()); };
+    if (xz.split_ws) {  // head-packed pieces: under the pairs layout (knob 2: under the halves too)
+        const bool hp = variant != 1 && use_head_pack_split(p, C, xa) && (knobs().head_pack == 2 || pairs_of(true));
+        xz.head_pack = hp ? 1 : 0;
+        xz.split_pairs = pairs_of(hp) ? 1 : 0;
+    } else {
+        xz.head_pack = variant != 1 && use_head_pack(p, C, xa) ? 1 : 0;
+        xz.split_pairs = 0;
+    }
+    xz.zigzag = !xz.split_ws && !xz.head_pack && variant != 1 && use_zigzag(p, C, xa) ? 1 : 0;
+    const int64_t n_plain = qtiles_of(xz.head_pack != 0);
     const int64_t heads_u = xz.head_pack ? p.num_heads_q / 4 : p.num_heads_q;
-    xz.split_pairs = xz.split_ws && use_split_pairs(n_plain * heads_u * p.batch_size, heads_u * p.batch_size,
-                                                    device_cus()) ? 1 : 0;
     const int64_t n_pairs = (n_plain + 1) / 2 * heads_u * p.batch_size;
     const int64_t n_qtiles = xz.split_ws ? 2 * n_plain : xz.zigzag ? zigzag_qtiles(p.seqlen_q) : n_plain;
     const int64_t nwg = n_qtiles * heads_u * p.batch_size;

@@ -166,28 +166,31 @@ inline bool use_head_pack(const fa_fwd_params &p, bool causal, const PathArgs &x
 }
 
 // Head-packed key-split pieces (fa_fwd_w4 "Head-packed blocks" + "key-split blocks"): a key-split
-// launch (one-round grid, use_split) with a multiple of 4 q-heads per kv-head runs its pieces over
+// launch (one-round grid, use_split) with a multiple of 4 q-heads per kv-head can run its pieces over
 // (batch, q-head quad, 64-row q-tile) blocks -- the halves or pairs layout over those units, the same
 // hand-off per (block, wave) (each wave one q-head's 64 rows, as a plain block's wave) -- so a piece's
-// diagonal is one tile. Knob head_pack: 0 never, 1 and 2 wherever this applies.
+// diagonal is one tile. Whether it may (launch_one decides): knob head_pack 1 (default) only under the
+// pairs layout (measured +0.8 to +7 % over plain-block pairs; under the halves it lost 1.5-14 %,
+// profiles/r6_split_rule_sweep.log), 2 under both, 0 never.
 inline bool use_head_pack_split(const fa_fwd_params &p, bool causal, const PathArgs &xa) {
     return causal && !xa.k_rng && !xa.cos && xa.window_left < 0 && knobs().head_pack != 0 &&
            p.head_q_per_group % 4 == 0 && p.seqlen_q > 64;
 }
 
 // Key-split causal blocks: dense causal launches (no varlen, window or RoPE) when the caller passes
-// the workspace. Knob 1 (default): where measured faster than zigzag (profiles/r4_split_sweep.log,
-// same-process A/B): the plain blocks fit one round of the grid and the keys are long enough for
-// each half to carry the piece's extra block start and combine -- at least 3072 keys, or 2048 when
-// the plain blocks fill at most half the CUs (+12 to +44 %; a full round at 1024-2048 keys lost
-// 9-26 %). Knob 2: always (tests). Workspace: the per-(block, wave) sync counters, then per (block,
+// the workspace. Knob 1 (default): where measured faster than zigzag (same-process A/B over one-round
+// grids, profiles/r6_split_rule_sweep.log; round 4's rule, before the pairs layout, was 3072 / 2048
+// keys): the plain blocks fit one round of the grid and the keys are long enough for each piece to
+// carry its extra block start and combine -- at least 2048 keys (more than half the CUs: the pairs
+// layout, +10 to +16 % at 2048; at 1024 MHA lost 8 %), or 1024 when the blocks fill at most half
+// the CUs (the halves, +6 to +14 % at 1024; at 512-768 zigzag ties or wins). Knob 2: always (tests). Workspace: the per-(block, wave) sync counters, then per (block,
 // wave) the partial O of its 64 rows (32 * DTL fp32 per lane) and two 16-byte statistic records per lane.
 inline bool use_split(const fa_fwd_params &p, bool causal, const PathArgs &xa) {
     if (!causal || xa.k_rng || xa.cos || xa.window_left >= 0 || knobs().split == 0 || p.seqlen_q <= 128) return false;
     if (!same_xcd_placement()) return false;  // (the pieces' hand-off needs one XCD per pair)
     if (knobs().split == 2) return true;
     const int64_t nwg = (p.seqlen_q + kBlockM - 1) / kBlockM * p.num_heads_q * p.batch_size, cus = device_cus();
-    return nwg <= cus && (p.seqlen_kv >= 3072 || (p.seqlen_kv >= 2048 && 2 * nwg <= cus));
+    return nwg <= cus && (p.seqlen_kv >= 2048 || (p.seqlen_kv >= 1024 && 2 * nwg <= cus));
 }
 constexpr int kSplitStatsPerLane = 8;  // floats: (nmsc, l) of blocks A and B, then (m_A, m_B, 0, 0)
 inline int64_t split_wave_floats(int64_t headdim) {

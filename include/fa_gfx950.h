@@ -114,7 +114,7 @@ int fa_fwd_gfx950(const fa_fwd_params *params, int dtype, int causal, void *stre
  * needs `workspace_bytes` >= fa_fwd_gfx950_workspace_size() of device memory
  * for fp32 partials. A causal prefill whose 256-row blocks fit one round of the
  * persistent grid (at most one block per CU: a single long sequence, one GPU's
- * share of a multi-GPU split) with at least 3072 keys (2048 when the blocks fill
+ * share of a multi-GPU split) with at least 2048 keys (1024 when the blocks fill
  * at most half the CUs) splits each block's keys in two pieces on two
  * workgroups instead, when the workspace holds at least
  * fa_fwd_gfx950_workspace_size() bytes (else the blocks run unsplit, in zigzag

@@ -461,17 +461,28 @@ def test_key_split_pairs(device, shape):
 
 def test_key_split_pairs_by_default_on_the_c4_share(device):
     """The default rule sends C4's 8-way share (B1 Hq16 Hkv4 S4096 causal) to key-split pairs over
-    head-packed blocks."""
+    head-packed blocks; a half-round grid (B1 Hq8 Hkv2 S4096: the halves layout) keeps plain blocks
+    (head-packed halves measured slower, profiles/r6_split_rule_sweep.log); key-split from 1024 keys on
+    a half-round grid and from 2048 on a fuller one, zigzag below."""
     import flash_attention_cute_amd as m
     from flash_attention_cute_amd import _debug
 
-    q, k, v = (torch.randn(1, h, 4096, 128, device=device, dtype=torch.float16) for h in (16, 4, 4))
+    def run(b, hq, hkv, s):
+        q, k, v = (torch.randn(b, h, s, 128, device=device, dtype=torch.float16) for h in (hq, hkv, hkv))
+        m.flash_attn_func(q, k, v, causal=True)
+        return _debug.last_layout(), _debug.last_split_pairs(), _debug.last_head_pack()
+
     _debug.set_knobs()
     _debug.set_split()
     _debug.set_split_pairs()
     _debug.set_head_pack()
-    m.flash_attn_func(q, k, v, causal=True)
-    assert _debug.last_layout() == "split" and _debug.last_split_pairs() and _debug.last_head_pack()
+    assert run(1, 16, 4, 4096) == ("split", True, True)
+    assert run(1, 8, 2, 4096) == ("split", False, False)
+    assert run(1, 32, 8, 2048) == ("split", True, True)  # 256 blocks, 2048 keys
+    assert run(1, 32, 32, 2048) == ("split", True, False)  # MHA: plain-block pairs
+    assert run(1, 16, 4, 1024) == ("split", False, False)  # 64 blocks: the halves from 1024 keys
+    assert run(2, 32, 8, 1024)[0] == "zigzag"  # 256 blocks of 1024 keys
+    assert run(1, 16, 4, 768)[0] == "zigzag"
 
 
 HP_SPLIT = [  # (B, Hq, Hkv, Sq, Sk, D): one-round causal GQA grids, g % 4 == 0
@@ -487,7 +498,8 @@ HP_SPLIT = [  # (B, Hq, Hkv, Sq, Sk, D): one-round causal GQA grids, g % 4 == 0
 @pytest.mark.parametrize("pairs", [1, 0], ids=["pairs", "halves"])
 def test_head_packed_key_split(device, shape, pairs):
     """Key-split pieces over head-packed blocks (fa_launch.h use_head_pack_split: the halves or pairs
-    layout over (batch, q-head quad, 64-row q-tile) units, one hand-off per (block, wave)): against the
+    layout over (batch, q-head quad, 64-row q-tile) units, one hand-off per (block, wave); knob 2, as
+    the default rule takes them under the pairs layout only): against the
     oracle, two launches and a capped persistent grid bit-identical, no hand-off error, close to the
     plain-block key-split layout (different split points: summation order only)."""
     import flash_attention_cute_amd as m
@@ -500,7 +512,7 @@ def test_head_packed_key_split(device, shape, pairs):
     _debug.set_knobs()
     _debug.set_split(2)
     _debug.set_split_pairs(pairs)
-    _debug.set_head_pack()
+    _debug.set_head_pack(2)  # (the default rule head-packs the pairs layout only)
     m.split_errors(reset=True)
     try:
         out = m.flash_attn_func(qd, kd, vd, causal=True)
@@ -566,10 +578,11 @@ def test_key_split_only_with_a_workspace(device):
         torch.cuda.synchronize()
         assert torch.equal(o, o3)
         assert (o.float() - o2.float()).abs().max().item() < 4e-3
-        # default knob: 8 x 32 heads x 4 q-tiles = 1024 blocks, four rounds, and this one-round 1024-key
-        # launch ask for none; 8 heads x 16 q-tiles of 4096 keys (128 blocks) does (contiguous strides)
+        # default knob: 8 x 32 heads x 4 q-tiles = 1024 blocks, four rounds, and a one-round 768-key
+        # launch ask for none; this one-round 1024-key launch (16 blocks) and 8 heads x 16 q-tiles of
+        # 4096 keys (128 blocks) do (contiguous strides)
         _debug.set_split()
-        assert lib.fa_fwd_gfx950_workspace_size(ctypes.byref(p), 0, 1) == 0
+        assert lib.fa_fwd_gfx950_workspace_size(ctypes.byref(p), 0, 1) > 0
 
         def params(b, hq, hkv, s):
             hs = {"q": hq, "k": hkv, "v": hkv, "o": hq}
@@ -577,6 +590,7 @@ def test_key_split_only_with_a_workspace(device):
             return _debug.FaFwdParams(0x10000, 0x10000, 0x10000, 0x10000, b, hq, hkv, s, s, 128, 4, *strides, 0.1)
 
         assert lib.fa_fwd_gfx950_workspace_size(ctypes.byref(params(8, 32, 8, 1024)), 0, 1) == 0
+        assert lib.fa_fwd_gfx950_workspace_size(ctypes.byref(params(1, 8, 2, 768)), 0, 1) == 0
         assert lib.fa_fwd_gfx950_workspace_size(ctypes.byref(params(1, 8, 2, 4096)), 0, 1) > 0
     finally:
         _debug.set_split()
@@ -628,7 +642,7 @@ def test_key_split_timeout_leaves_the_next_launch_correct(device, layout):
     dl = _debug.lib(debug=True)
     _debug.set_split(2, debug=True)
     _debug.set_split_pairs(1 if pairs else 0, debug=True)
-    _debug.set_head_pack(1 if hp else 0, debug=True)
+    _debug.set_head_pack(2 if hp else 0, debug=True)
     dl.fa_split_errors(1)
     try:
         _debug.set_split_fault(True)
@@ -778,6 +792,7 @@ def test_head_packed_blocks(device, shape, dtype):
     q, k, v = make(b, hq, hkv, sq, sk, d, dtype, zlib.crc32(repr((shape, str(dtype), "hp")).encode()))
     qd, kd, vd = q.to(device), k.to(device), v.to(device)
     _debug.set_knobs()
+    _debug.set_split(0)  # (one-round shapes of 1024+ keys take key-split by default)
     try:
         _debug.set_head_pack(2)
         out = m.flash_attn_func(qd, kd, vd, causal=True)

@@ -52,10 +52,12 @@ def op(device, request):
     _debug.set_knobs(w4_grid=16)
     if request.param == "w4hp":  # (g = 4: every causal launch below runs head-packed blocks)
         _debug.set_head_pack(2)
-    if request.param == "w4hpsplit":
+        _debug.set_split(0)  # (the shape's one-round grid would take key-split by default: w4hpsplit)
+    if request.param == "w4hpsplit":  # (the capped grid runs the halves: head-packed under knob 2)
         import flash_attention_cute_amd as m
 
         _debug.set_split(2)
+        _debug.set_head_pack(2)
         m.split_errors(reset=True)
     try:
         yield _Op(request.param)
