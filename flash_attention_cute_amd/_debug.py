@@ -67,6 +67,8 @@ def lib(debug: bool = False) -> ctypes.CDLL:
         lib.fa_debug_set_split_fault.restype = None
         lib.fa_debug_last_dec_fused.restype = ctypes.c_int
         lib.fa_debug_set_head_pack.argtypes = [ctypes.c_int]
+        lib.fa_debug_set_split_rr.argtypes = [ctypes.c_int]
+        lib.fa_debug_set_split_rr.restype = None
         lib.fa_debug_set_head_pack.restype = None
         lib.fa_fwd_gfx950_workspace_size.restype = ctypes.c_int64
         lib.fa_fwd_gfx950_ws.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
@@ -125,6 +127,12 @@ def set_split_pairs(mode: int | None = None, debug: bool = False) -> None:
     """Key-split pairs (a heavy and a light q-tile on two workgroups, one pass; fa_launch.h
     use_split_pairs): 0 never, 1 where they fit one pass of the grid (the default); None restores it."""
     lib(debug).fa_debug_set_split_pairs(-1 if mode is None else int(mode))
+
+
+def set_split_rr(mode: int | None = None, debug: bool = False) -> None:
+    """Work order of the key-split halves: 1 level-major (every XCD a share of every q-tile level, the
+    default), 0 decode_work's XCD-contiguous ranges; None restores the default."""
+    lib(debug).fa_debug_set_split_rr(-1 if mode is None else int(mode))
 
 
 def set_dec_fuse(mode: int | None = None, debug: bool = False) -> None:

@@ -37,7 +37,7 @@ unsigned long long *g_stamps = nullptr;
 thread_local int g_last_path = fa::kPathNone;
 
 fa::Knobs knobs_from_env() {
-    fa::Knobs k{0, 0, 1, fa::kDecTargetWgs, fa::kDecNt, 1, 1, FA_SPLIT_PAIRS, FA_DEC_FUSE, 0, FA_HEAD_PACK, 0};
+    fa::Knobs k{0, 0, 1, fa::kDecTargetWgs, fa::kDecNt, 1, 1, FA_SPLIT_PAIRS, FA_DEC_FUSE, 0, FA_HEAD_PACK, 0, FA_SPLIT_RR};
     if (const char *v = getenv("FA_GFX950_VARIANT"))
         k.variant = !strcmp(v, "w8") ? 1 : !strcmp(v, "w4slow") ? 2 : !strcmp(v, "p8") ? 3 : !strcmp(v, "m32") ? 4
                   : !strcmp(v, "m16") ? 5 : 0;
@@ -51,6 +51,7 @@ fa::Knobs knobs_from_env() {
     if (const char *e = getenv("FA_DEC_FUSE")) k.dec_fuse = atoi(e);
     if (const char *e = getenv("FA_XCCS")) k.xccs = atoi(e) > 0 ? atoi(e) : 0;
     if (const char *e = getenv("FA_HEAD_PACK")) k.head_pack = atoi(e);
+    if (const char *e = getenv("FA_SPLIT_RR")) k.split_rr = atoi(e);
 #ifdef FA_DEBUG_VARIANTS
     if (k.variant != 0)  // a debug / A-B body replaces the product kernel for the whole process: say so
         fprintf(stderr,
@@ -121,6 +122,11 @@ extern "C" void fa_debug_set_dec_fuse(int mode) {
 // placement knob (Knobs::xccs, env FA_XCCS): XCDs per device for same_xcd_placement (0 / < 0: the
 // device's own count) -- tests force a count that does not divide 8 to see the fallback layouts
 extern "C" void fa_debug_set_xccs(int n) { knobs_mut().xccs = n < 0 ? env_defaults().xccs : n; }
+// key-split halves' work order knob (Knobs::split_rr, env FA_SPLIT_RR): 0 the XCD-contiguous
+// decode_work ranges, 1 level-major (every XCD a share of every q-tile level); < 0 restores the default
+extern "C" void fa_debug_set_split_rr(int mode) {
+    knobs_mut().split_rr = mode < 0 ? env_defaults().split_rr : mode;
+}
 // (debug library only) force one key-split hand-off per launch to time out (slot 0, wave 0; fa_fwd_w4
 // dbg & 2): 1 on, 0 off; the product library ignores it
 extern "C" void fa_debug_set_split_fault(int on) {

@@ -55,6 +55,7 @@ struct Knobs {
     int xccs;         // XCDs per device for the placement check (0: the device's own count; tests)
     int head_pack;    // head-packed causal GQA blocks (use_head_pack): 0 never, 1 the rule (default), 2 always
     int split_fault;  // (debug library only) force one key-split hand-off to time out (kernel dbg & 2)
+    int split_rr;     // key-split halves' order: 0 XCD-contiguous decode_work ranges, 1 level-major (default)
 };
 
 const Knobs &knobs();
@@ -133,6 +134,7 @@ struct PathArgs {
     unsigned *split_err;
     int split_pairs;
     int head_pack;  // (set by launch_one, use_head_pack) head-packed causal blocks (fa_fwd_w4)
+    int split_rr;   // (set by launch_one, knob split_rr) the halves' units level-major over the XCDs
 };
 
 // Whether a prefill launch runs zigzag Q blocks, and its logical q-tile count (blocks per (batch,
@@ -206,6 +208,9 @@ inline int64_t split_wave_floats(int64_t headdim) {
 #endif
 #ifndef FA_HEAD_PACK  // default of Knobs::head_pack
 #define FA_HEAD_PACK 1
+#endif
+#ifndef FA_SPLIT_RR  // default of Knobs::split_rr (level-major halves: +1.7 to +4.6 %, r6_ab_split_halves_order.log)
+#define FA_SPLIT_RR 1
 #endif
 #ifndef FA_DEC_FUSE  // default of Knobs::dec_fuse
 #define FA_DEC_FUSE 1

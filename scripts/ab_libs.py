@@ -4,7 +4,7 @@ same device, same inputs), so device-to-device clock differences cancel out.
 usage: python scripts/ab_libs.py <cfg> <lib.so>[@variant[:knob=value,...]] [...]   (env AB_REPS, AB_ITERS)
        variant: w4 | w8 | w4slow | p8 | m32 | m16, set through the library's fa_debug_set_knobs before its runs;
        knobs (debug setters of that library, applied before its runs): hp (head-packed blocks), zz (zigzag),
-       split, pairs. A library named twice is loaded from a copy, so each entry keeps its own knobs.
+       split, pairs, rr. A library named twice is loaded from a copy, so each entry keeps its own knobs.
 """
 import ctypes
 import os
@@ -24,7 +24,7 @@ if os.environ.get("AB_SHAPE"):  # B,Hq,Hkv,S,D,dtype,causal: a shape of its own 
     cfg.pop("W", None)
 VARIANTS = {"w4": 0, "w8": 1, "w4slow": 2, "p8": 3, "m32": 4, "m16": 5}
 SETTERS = {"hp": "fa_debug_set_head_pack", "zz": "fa_debug_set_zigzag", "split": "fa_debug_set_split",
-           "pairs": "fa_debug_set_split_pairs"}
+           "pairs": "fa_debug_set_split_pairs", "rr": "fa_debug_set_split_rr"}
 specs = [a.split("@") for a in sys.argv[2:]]
 libs, seen = [], set()
 for i, sp in enumerate(specs):

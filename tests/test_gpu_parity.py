@@ -540,6 +540,38 @@ def test_head_packed_key_split(device, shape, pairs):
     assert (out.float() - plain.float()).abs().max().item() < tol
 
 
+@pytest.mark.parametrize("hp", [0, 2], ids=["plain", "headpack"])
+def test_key_split_halves_order_is_bit_identical(device, hp):
+    """The halves' work order (knob split_rr: level-major, the default, or decode_work's XCD-contiguous
+    ranges) moves pieces between workgroups only: the split points and the order-independent combine
+    are the same, so the outputs are bit-identical; no hand-off error either way."""
+    import flash_attention_cute_amd as m
+    from flash_attention_cute_amd import _debug
+
+    q, k, v = (t.to(device) for t in make(1, 8, 2, 2048, 2048, 128, torch.bfloat16, 41))
+    _debug.set_knobs()
+    _debug.set_split(2)
+    _debug.set_split_pairs(0)
+    _debug.set_head_pack(hp)
+    m.split_errors(reset=True)
+    try:
+        outs = []
+        for rr in (1, 0):
+            _debug.set_split_rr(rr)
+            outs.append(m.flash_attn_func(q, k, v, causal=True))
+            assert _debug.last_layout() == "split" and not _debug.last_split_pairs()
+            assert _debug.last_head_pack() == (hp == 2)
+        torch.cuda.synchronize()
+    finally:
+        _debug.set_split_rr()
+        _debug.set_split()
+        _debug.set_split_pairs()
+        _debug.set_head_pack()
+    assert torch.equal(outs[0], outs[1])
+    assert m.split_errors() == 0
+    check(outs[0], q.cpu(), k.cpu(), v.cpu(), 128 ** -0.5, True, torch.bfloat16)
+
+
 def test_key_split_only_with_a_workspace(device):
     """The C-ABI runs key-split blocks only when the caller passes the workspace
     fa_fwd_gfx950_workspace_size asks for (the torch op does); without one (plain fa_fwd_gfx950) the
