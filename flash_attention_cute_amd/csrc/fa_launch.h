@@ -153,7 +153,8 @@ inline int64_t zigzag_qtiles(int64_t seqlen_q) { return ((seqlen_q + 127) / 128 
 // Head-packed causal blocks (fa_fwd_w4 "Head-packed blocks"): causal GQA with a multiple of 4 q-heads
 // per kv-head (4 consecutive q-heads of one kv group per block, one per wave: Llama-3-8B's g = 4 --
 // C4, C5 -- or Llama-3-70B's g = 8 as two quads), more than one 64-row q-tile, when neither zigzag nor
-// key-split takes the launch (multi-round grids). Dense, fused-RoPE (the patched Llama layer),
+// key-split takes the launch (multi-round grids, and one-round grids more than half full). Dense,
+// fused-RoPE (the patched Llama layer),
 // per-sequence-range (varlen, padded) and local-window launches. A block is (batch, q-head quad,
 // 64 rows): its causal diagonal is one tile instead of the plain 256-row block's four, two of them
 // A-dead (and a window's left edge spans 64 rows' keys, not 256); bit-identical to the plain layout. Knob head_pack (env FA_HEAD_PACK): 0 never, 1 by this
@@ -163,8 +164,11 @@ inline bool use_head_pack(const fa_fwd_params &p, bool causal, const PathArgs &x
     if (p.head_q_per_group % 4 != 0 || p.seqlen_q <= 64) return false;
     if (knobs().head_pack == 2) return true;
     if (knobs().zigzag == 2 && use_zigzag(p, causal, xa)) return false;  // (a forced zigzag wins over the rule)
+    // multi-round grids, and one-round grids more than half full that key-split did not take (short keys):
+    // there head-packed blocks measured +4 to +6 % over zigzag (B4 Hq32 S512, B8 Hq32 S256) and tied at
+    // 192 blocks; at half fill or less zigzag ties or wins (profiles/r6_ab_headpack_short.log)
     const int64_t nwg = (p.seqlen_q + kBlockM - 1) / kBlockM * p.num_heads_q * p.batch_size;
-    return nwg > device_cus();
+    return 2 * nwg > device_cus();
 }
 
 // Head-packed key-split pieces (fa_fwd_w4 "Head-packed blocks" + "key-split blocks"): a key-split

@@ -921,9 +921,10 @@ def test_head_packed_blocks_on_rope_ranges_and_window(device, entry, dtype):
 
 
 def test_head_packed_blocks_by_default(device):
-    """The default rule: multi-round causal grids with g = 4 take head-packed blocks (C4 / C5's class);
-    g = 8 too (two q-head quads per kv group); g = 2, non-causal, and one-round grids (zigzag /
-    key-split) do not."""
+    """The default rule: multi-round causal grids with g = 4 take head-packed blocks (C4 / C5's class),
+    and one-round grids more than half full that key-split leaves (short keys); g = 8 too (two q-head
+    quads per kv group); g = 2, non-causal, half-full short grids (zigzag) and long one-round grids
+    (key-split) do not."""
     import flash_attention_cute_amd as m
     from flash_attention_cute_amd import _debug
 
@@ -947,4 +948,10 @@ def test_head_packed_blocks_by_default(device):
     assert _debug.last_layout() == "headpack"
     one = [torch.randn(1, h, 1024, 128, device=device, dtype=torch.float16) for h in (8, 2, 2)]  # 32 blocks
     m.flash_attn_func(*one, causal=True)
-    assert _debug.last_layout() in ("zigzag", "split")
+    assert _debug.last_layout() == "split"  # (1024 keys at half fill: key-split)
+    short = [torch.randn(2, h, 512, 128, device=device, dtype=torch.float16) for h in (32, 8, 8)]  # 128 blocks
+    m.flash_attn_func(*short, causal=True)
+    assert _debug.last_layout() == "zigzag"  # (half fill, short keys)
+    full = [torch.randn(4, h, 512, 128, device=device, dtype=torch.float16) for h in (32, 8, 8)]  # 256 blocks
+    m.flash_attn_func(*full, causal=True)
+    assert _debug.last_layout() == "headpack"  # (a full round of short keys)
