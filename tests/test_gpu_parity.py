@@ -463,7 +463,8 @@ def test_key_split_pairs_by_default_on_the_c4_share(device):
     """The default rule sends C4's 8-way share (B1 Hq16 Hkv4 S4096 causal) to key-split pairs over
     head-packed blocks; a half-round grid (B1 Hq8 Hkv2 S4096: the halves layout) keeps plain blocks
     (head-packed halves measured slower, profiles/r6_split_rule_sweep.log); key-split from 1024 keys on
-    a half-round grid and from 2048 on a fuller one, zigzag below."""
+    a half-round grid and from 2048 on a fuller one; below, zigzag at half fill or less and head-packed
+    blocks above."""
     import flash_attention_cute_amd as m
     from flash_attention_cute_amd import _debug
 
@@ -481,7 +482,7 @@ def test_key_split_pairs_by_default_on_the_c4_share(device):
     assert run(1, 32, 8, 2048) == ("split", True, True)  # 256 blocks, 2048 keys
     assert run(1, 32, 32, 2048) == ("split", True, False)  # MHA: plain-block pairs
     assert run(1, 16, 4, 1024) == ("split", False, False)  # 64 blocks: the halves from 1024 keys
-    assert run(2, 32, 8, 1024)[0] == "zigzag"  # 256 blocks of 1024 keys
+    assert run(2, 32, 8, 1024)[0] == "headpack"  # 256 blocks of 1024 keys: no key-split, a full round
     assert run(1, 16, 4, 768)[0] == "zigzag"
 
 
